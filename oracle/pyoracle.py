@@ -1,0 +1,118 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes front-end for oracle/build/liboracle.so.
+
+The checker for the HIP path (never the thing measured as the product, never shipped).
+Built from oracle/xsalsa_oracle.c by oracle/Makefile (see that file's header for the
+reference file:line each function restates).
+"""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBPATH = os.path.join(HERE, "build", "liboracle.so")
+
+BLOCK_DATA = 65536
+BLOCK_SIZE = 65552
+FILE_HDR = 32
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def _load():
+    if not os.path.exists(LIBPATH):
+        build()
+    lib = ctypes.CDLL(LIBPATH)
+    c_p = ctypes.c_char_p
+    vp = ctypes.c_void_p
+    lib.orc_secretbox_seal.argtypes = [vp, vp, ctypes.c_size_t, c_p, c_p]
+    lib.orc_secretbox_open.argtypes = [vp, vp, ctypes.c_size_t, c_p, c_p]
+    lib.orc_secretbox_open.restype = ctypes.c_int
+    lib.orc_hsalsa20.argtypes = [vp, c_p, c_p]
+    lib.orc_salsa20_block.argtypes = [vp, c_p, c_p, ctypes.c_uint64]
+    lib.orc_poly1305.argtypes = [vp, vp, ctypes.c_size_t, c_p]
+    lib.orc_nonce_increment.argtypes = [vp]
+    lib.orc_nonce_add.argtypes = [vp, ctypes.c_uint64]
+    lib.orc_encrypted_size.argtypes = [ctypes.c_int64]
+    lib.orc_encrypted_size.restype = ctypes.c_int64
+    lib.orc_decrypted_size.argtypes = [ctypes.c_int64]
+    lib.orc_decrypted_size.restype = ctypes.c_int64
+    lib.orc_calculate_underlying.argtypes = [ctypes.c_int64, ctypes.c_int64, vp]
+    lib.orc_encrypt_file.argtypes = [vp, vp, ctypes.c_int64, c_p, c_p]
+    lib.orc_decrypt_file.argtypes = [vp, vp, ctypes.c_int64, c_p, ctypes.c_int, vp]
+    lib.orc_decrypt_file.restype = ctypes.c_int64
+    lib.orc_seal_blocks.argtypes = [vp, vp, ctypes.c_int64, c_p, c_p]
+    lib.orc_seal_blocks.restype = ctypes.c_int
+    lib.orc_open_blocks.argtypes = [vp, vp, vp, ctypes.c_int64, c_p, c_p]
+    lib.orc_open_blocks.restype = ctypes.c_int
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _load()
+    return _lib
+
+
+def _buf(b):
+    return ctypes.create_string_buffer(bytes(b), len(b)) if len(b) else ctypes.create_string_buffer(1)
+
+
+def seal(msg: bytes, nonce: bytes, key: bytes) -> bytes:
+    out = ctypes.create_string_buffer(len(msg) + 16)
+    lib().orc_secretbox_seal(out, _buf(msg), len(msg), nonce, key)
+    return out.raw
+
+
+def open_box(box: bytes, nonce: bytes, key: bytes):
+    out = ctypes.create_string_buffer(max(len(box) - 16, 1))
+    rc = lib().orc_secretbox_open(out, _buf(box), len(box), nonce, key)
+    return out.raw[: len(box) - 16] if rc == 0 else None
+
+
+def nonce_increment(n: bytes) -> bytes:
+    b = ctypes.create_string_buffer(bytes(n), 24)
+    lib().orc_nonce_increment(b)
+    return b.raw
+
+
+def nonce_add(n: bytes, x: int) -> bytes:
+    b = ctypes.create_string_buffer(bytes(n), 24)
+    lib().orc_nonce_add(b, x)
+    return b.raw
+
+
+def encrypted_size(n: int) -> int:
+    return lib().orc_encrypted_size(n)
+
+
+def decrypted_size(n: int) -> int:
+    return lib().orc_decrypted_size(n)
+
+
+def calculate_underlying(offset: int, limit: int):
+    out = (ctypes.c_int64 * 4)()
+    lib().orc_calculate_underlying(offset, limit, out)
+    return tuple(out)
+
+
+def encrypt_file(plain: bytes, nonce0: bytes, key: bytes) -> bytes:
+    out = ctypes.create_string_buffer(encrypted_size(len(plain)))
+    lib().orc_encrypt_file(out, _buf(plain), len(plain), nonce0, key)
+    return out.raw
+
+
+def decrypt_file(ct: bytes, key: bytes, pass_bad_blocks=False):
+    """Returns (plaintext or None, code) with code 0 ok, -1 too short, -2 bad magic,
+    -3 truncated block header, -4 bad block (first bad block index in the tuple)."""
+    out = ctypes.create_string_buffer(max(len(ct), 1))
+    bad = ctypes.c_int64(-1)
+    rc = lib().orc_decrypt_file(out, _buf(ct), len(ct), key, int(pass_bad_blocks), ctypes.byref(bad))
+    if rc < 0:
+        return None, rc, bad.value
+    return out.raw[:rc], 0, -1
