@@ -1,0 +1,193 @@
+/*
+ * rclone_crypt_gpu.h -- C ABI of the MI355X (gfx950) crypt-overlay data path.
+ *
+ * Drop-in boundary for rclone's backend/crypt data cipher (reference v1.76.0,
+ * /root/reference).  Two layers, both plain C (pointers + sizes, no torch/HIP types):
+ *
+ *  1. xs_*  -- the primitive seam.  Batched NaCl secretbox over crypt blocks, replacing the
+ *     per-block calls secretbox.Seal (backend/crypt/cipher.go:737) and secretbox.Open
+ *     (cipher.go:880) of x/crypto v0.54.0.  Block i of an object uses nonce0 + i
+ *     (nonce.add, cipher.go:665-678).  Wire layout of a block: tag(16) || ciphertext(n),
+ *     blocks back to back with stride 65552 (cipher.go:39-40, EncryptedSize :1121).
+ *     *_dev entry points take device pointers and a hipStream_t passed as void*.
+ *     xs_engine_* take host pointers (pinned via xs_host_alloc for full speed) and
+ *     overlap H2D / kernels / D2H on side streams.
+ *
+ *  2. rc_*  -- the cipher.go data API itself (Cipher, EncryptData, DecryptData,
+ *     DecryptDataSeek, RangeSeek, EncryptedSize, DecryptedSize, nonce arithmetic) with the
+ *     same argument meaning, error values and error precedence, io.Reader expressed as
+ *     a C callback.  This is what a cgo binding of backend/crypt would call.
+ *
+ * Thread safety: xs_*_dev are reentrant (callers own workspace and stream); an xs_engine
+ * serialises its own calls; rc_* handles serialise per handle like the reference's fh.mu
+ * (cipher.go:682, :778) and may be used from many threads at once.
+ */
+#ifndef RCLONE_CRYPT_GPU_H
+#define RCLONE_CRYPT_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XS_BLOCK_DATA 65536u /* blockDataSize cipher.go:39 */
+#define XS_BLOCK_HDR 16u     /* blockHeaderSize = secretbox.Overhead cipher.go:38 */
+#define XS_BLOCK_SIZE 65552u /* blockSize cipher.go:40 */
+#define XS_FILE_HDR 32u      /* fileHeaderSize cipher.go:37 */
+
+/* xs_* return codes */
+#define XS_OK 0
+#define XS_ERR_INVALID (-1) /* bad argument / size / alignment */
+#define XS_ERR_HIP (-2)     /* HIP runtime error (see xs_last_error) */
+#define XS_ERR_NOMEM (-3)
+#define XS_ERR_NODEV (-4)
+
+/* One crypt block of a batch (descriptor mode).  Offsets are bytes from the src / dst
+ * base pointers.  Seal: src_off -> plaintext, dst_off -> wire block (tag first).
+ * Open: src_off -> wire block (tag first), dst_off -> plaintext.  len = plaintext bytes
+ * (1..65536).  Payload addresses (plaintext and ciphertext = wire + 16) must be 16-byte
+ * aligned. */
+typedef struct xs_block_desc {
+  uint64_t src_off;
+  uint64_t dst_off;
+  uint32_t len;
+  uint32_t reserved;
+  uint8_t nonce[24];
+} xs_block_desc;
+
+const char *xs_version(void);
+/* Last error message of the calling thread ("" if none). */
+const char *xs_last_error(void);
+/* Number of HIP devices (0 when none; never fails). */
+int xs_device_count(void);
+/* Device workspace bytes needed for a batch of nblocks (per-block key schedule). */
+size_t xs_workspace_bytes(uint64_t nblocks);
+
+/* Seal a contiguous plaintext object range: blocks first_block.. of an object whose block 0
+ * uses nonce0.  d_plain holds plain_len bytes (block i at i*65536); d_body receives the
+ * wire blocks (block i at i*65552; EncryptedSize(plain_len)-32 bytes for a whole object).
+ * Replaces the secretbox.Seal loop of encrypter.Read (cipher.go:719-745). */
+int xs_seal_object_dev(const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                       const void *d_plain, uint64_t plain_len, void *d_body, void *d_workspace,
+                       void *stream);
+/* Open wire blocks (body_len bytes, block i at i*65552) into d_plain (block i at i*65536).
+ * d_ok[i] = 1 if block i authenticated, else 0 and that block's plaintext is zero-filled
+ * (secretbox.Open failure, cipher.go:880-893).  Every block must hold > 16 bytes. */
+int xs_open_object_dev(const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                       const void *d_body, uint64_t body_len, void *d_plain, uint8_t *d_ok,
+                       void *d_workspace, void *stream);
+/* Descriptor mode: d_desc is a device array of nblocks descriptors; src/dst buffers are
+ * src_len/dst_len bytes.  A descriptor that is out of bounds, misaligned or has len outside
+ * 1..65536 is skipped on the device (nothing written; d_ok[i] = 0 when opening), so a bad
+ * descriptor can never fault the GPU. */
+int xs_seal_batch_dev(const uint8_t key[32], const xs_block_desc *d_desc, uint64_t nblocks,
+                      const void *d_src, uint64_t src_len, void *d_dst, uint64_t dst_len,
+                      void *d_workspace, void *stream);
+int xs_open_batch_dev(const uint8_t key[32], const xs_block_desc *d_desc, uint64_t nblocks,
+                      const void *d_src, uint64_t src_len, void *d_dst, uint64_t dst_len, uint8_t *d_ok,
+                      void *d_workspace, void *stream);
+/* Fill d with the SplitMix64 stream (word k = mix(seed + (k+1)*0x9E3779B97F4A7C15)). */
+int xs_fill_random_dev(void *d, uint64_t nbytes, uint64_t seed, void *stream);
+
+/* Host-memory engine: pinned staging, per-slot streams, H2D/kernel/D2H overlapped. */
+typedef struct xs_engine xs_engine;
+xs_engine *xs_engine_create(int device, uint32_t batch_blocks, int nslots);
+void xs_engine_destroy(xs_engine *e);
+int xs_engine_seal(xs_engine *e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                   const void *plain, uint64_t plain_len, void *body);
+int xs_engine_open(xs_engine *e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                   const void *body, uint64_t body_len, void *plain, uint8_t *ok);
+/* Pinned (page-locked) host memory. */
+void *xs_host_alloc(size_t bytes);
+void xs_host_free(void *p);
+
+/* ------------------------------------------------------------------------------------
+ * rc_*: backend/crypt/cipher.go data API.
+ * Error values (int32): RC_NIL, RC_EOF (io.EOF), RC_UNEXPECTED_EOF (io.ErrUnexpectedEOF),
+ * the crypt sentinels below (cipher.go:44-58), or any value >= RC_USER_BASE produced by a
+ * caller's reader / opener, which is passed through unchanged exactly where the
+ * reference passes the underlying error through.
+ * ---------------------------------------------------------------------------------- */
+#define RC_NIL 0
+#define RC_EOF 1
+#define RC_UNEXPECTED_EOF 2
+#define RC_USER_BASE 16
+#define RC_ERR_FILE_TOO_SHORT (-101) /* ErrorEncryptedFileTooShort */
+#define RC_ERR_FILE_BAD_HEADER (-102) /* ErrorEncryptedFileBadHeader */
+#define RC_ERR_BAD_MAGIC (-103)       /* ErrorEncryptedBadMagic */
+#define RC_ERR_BAD_BLOCK (-104)       /* ErrorEncryptedBadBlock */
+#define RC_ERR_FILE_CLOSED (-105)     /* ErrorFileClosed */
+#define RC_ERR_BAD_SEEK (-106)        /* ErrorBadSeek */
+#define RC_ERR_SHORT_NONCE (-107)     /* "short read of nonce: %w" (cipher.go:633) */
+#define RC_ERR_SEEK_NOT_INIT (-108)   /* "can't seek - not initialised with newDecrypterSeek" */
+#define RC_ERR_SEEK_WHENCE (-109)     /* "can only seek from the start" */
+#define RC_ERR_REOPEN (-110)          /* "couldn't reopen file with offset and limit: %w" */
+#define RC_ERR_GPU (-120)             /* device failure (xs_last_error has the reason) */
+#define RC_ERR_INVALID (-121)
+
+/* io.Reader: read up to n bytes into p, return the count (>= 0) and set *err. */
+typedef int64_t (*rc_read_fn)(void *user, uint8_t *p, int64_t n, int32_t *err);
+/* io.Closer */
+typedef int32_t (*rc_close_fn)(void *user);
+/* optional fs.RangeSeeker (fs/types.go, used at cipher.go:997) */
+typedef int32_t (*rc_range_seek_fn)(void *user, int64_t offset, int32_t whence, int64_t limit);
+typedef struct rc_reader {
+  rc_read_fn read;
+  rc_close_fn close;           /* may be NULL (io.NopCloser) */
+  rc_range_seek_fn range_seek; /* may be NULL */
+  void *user;
+} rc_reader;
+/* OpenRangeSeek (cipher.go:77): open the underlying object at (offset, limit). */
+typedef int32_t (*rc_open_fn)(void *user, int64_t offset, int64_t limit, rc_reader *out);
+
+typedef struct rc_cipher rc_cipher;
+typedef struct rc_encrypter rc_encrypter;
+typedef struct rc_decrypter rc_decrypter;
+
+/* newCipher + Key (cipher.go:187, :231): scrypt(N=16384,r=8,p=1) key derivation; empty
+ * password -> all-zero keys; empty salt -> built-in defaultSalt. */
+rc_cipher *rc_cipher_new(const char *password, const char *salt, int32_t *err);
+int32_t rc_cipher_key(rc_cipher *c, const char *password, const char *salt);
+void rc_cipher_keys(const rc_cipher *c, uint8_t data_key[32], uint8_t name_key[32], uint8_t name_tweak[16]);
+void rc_cipher_set_pass_bad_blocks(rc_cipher *c, int32_t pass); /* setPassBadBlocks :217 */
+void rc_cipher_set_rand(rc_cipher *c, rc_reader rand);           /* c.cryptoRand */
+/* Blocks staged per GPU submission by encrypters/decrypters (default 64 = 4 MiB). */
+void rc_cipher_set_batch_blocks(rc_cipher *c, uint32_t blocks);
+void rc_cipher_free(rc_cipher *c);
+
+int64_t rc_encrypted_size(int64_t size);               /* EncryptedSize :1121 */
+int64_t rc_decrypted_size(int64_t size, int32_t *err); /* DecryptedSize :1131 */
+void rc_calculate_underlying(int64_t offset, int64_t limit, int64_t out[4]); /* :935 */
+void rc_nonce_increment(uint8_t nonce[24]);            /* :660 */
+void rc_nonce_add(uint8_t nonce[24], uint64_t x);      /* :665 */
+
+/* newEncrypter (cipher.go:694) / EncryptData (:771).  nonce NULL -> read 24 bytes from the
+ * cipher's random source.  On error returns NULL and sets *err. */
+rc_encrypter *rc_encrypt_data(rc_cipher *c, rc_reader in, const uint8_t *nonce, int32_t *err);
+int64_t rc_encrypter_read(rc_encrypter *e, uint8_t *p, int64_t n, int32_t *err); /* :719 */
+void rc_encrypter_nonce(const rc_encrypter *e, uint8_t out[24]);
+void rc_encrypter_free(rc_encrypter *e);
+
+/* newDecrypter / DecryptData (:793, :1099) */
+rc_decrypter *rc_decrypt_data(rc_cipher *c, rc_reader rc, int32_t *err);
+/* DecryptDataSeek (:1112) */
+rc_decrypter *rc_decrypt_data_seek(rc_cipher *c, rc_open_fn open, void *open_user, int64_t offset,
+                                   int64_t limit, int32_t *err);
+int64_t rc_decrypter_read(rc_decrypter *d, uint8_t *p, int64_t n, int32_t *err); /* :901 */
+int64_t rc_decrypter_range_seek(rc_decrypter *d, int64_t offset, int32_t whence, int64_t limit,
+                                int32_t *err);                                   /* :972 */
+int32_t rc_decrypter_close(rc_decrypter *d);                                     /* :1069 */
+void rc_decrypter_nonce(const rc_decrypter *d, uint8_t out[24]);
+/* error wrapped by RC_ERR_REOPEN / RC_ERR_SHORT_NONCE (the %w operand) */
+int32_t rc_decrypter_wrapped_error(const rc_decrypter *d);
+void rc_decrypter_free(rc_decrypter *d);
+
+/* Message of an rc_* error value (the reference's error string). */
+const char *rc_error_string(int32_t err);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

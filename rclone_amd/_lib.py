@@ -1,0 +1,111 @@
+"""ctypes binding of rclone_amd/librclone_crypt.so (include/rclone_crypt_gpu.h).
+
+There is no fallback: if the native library is missing or has no GPU, calls fail loudly.
+"""
+import ctypes
+import os
+
+from . import build as _build
+
+_lib = None
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+vp = ctypes.c_void_p
+u64 = ctypes.c_uint64
+i64 = ctypes.c_int64
+i32 = ctypes.c_int32
+
+
+class XsBlockDesc(ctypes.Structure):
+    _fields_ = [("src_off", ctypes.c_uint64), ("dst_off", ctypes.c_uint64), ("len", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32), ("nonce", ctypes.c_uint8 * 24)]
+
+
+assert ctypes.sizeof(XsBlockDesc) == 48
+
+READ_FN = ctypes.CFUNCTYPE(i64, vp, c_u8p, i64, ctypes.POINTER(i32))
+CLOSE_FN = ctypes.CFUNCTYPE(i32, vp)
+RANGE_SEEK_FN = ctypes.CFUNCTYPE(i32, vp, i64, i32, i64)
+
+
+class RcReader(ctypes.Structure):
+    _fields_ = [("read", READ_FN), ("close", CLOSE_FN), ("range_seek", RANGE_SEEK_FN), ("user", vp)]
+
+
+OPEN_FN = ctypes.CFUNCTYPE(i32, vp, i64, i64, ctypes.POINTER(RcReader))
+
+# (name, restype, argtypes)
+_SIGS = [
+    ("xs_version", ctypes.c_char_p, []),
+    ("xs_last_error", ctypes.c_char_p, []),
+    ("xs_device_count", ctypes.c_int, []),
+    ("xs_workspace_bytes", ctypes.c_size_t, [u64]),
+    ("xs_seal_object_dev", ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, u64, vp, u64, vp, vp, vp]),
+    ("xs_open_object_dev", ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, u64, vp, u64, vp, vp, vp, vp]),
+    ("xs_seal_batch_dev", ctypes.c_int, [ctypes.c_char_p, vp, u64, vp, u64, vp, u64, vp, vp]),
+    ("xs_open_batch_dev", ctypes.c_int, [ctypes.c_char_p, vp, u64, vp, u64, vp, u64, vp, vp, vp]),
+    ("xs_fill_random_dev", ctypes.c_int, [vp, u64, u64, vp]),
+    ("xs_engine_create", vp, [ctypes.c_int, ctypes.c_uint32, ctypes.c_int]),
+    ("xs_engine_destroy", None, [vp]),
+    ("xs_engine_seal", ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, u64, vp, u64, vp]),
+    ("xs_engine_open", ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, u64, vp, u64, vp, vp]),
+    ("xs_host_alloc", vp, [ctypes.c_size_t]),
+    ("xs_host_free", None, [vp]),
+    # cipher.go mirror
+    ("rc_cipher_new", vp, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(i32)]),
+    ("rc_cipher_key", i32, [vp, ctypes.c_char_p, ctypes.c_char_p]),
+    ("rc_cipher_keys", None, [vp, vp, vp, vp]),
+    ("rc_cipher_set_pass_bad_blocks", None, [vp, i32]),
+    ("rc_cipher_set_rand", None, [vp, RcReader]),
+    ("rc_cipher_set_batch_blocks", None, [vp, ctypes.c_uint32]),
+    ("rc_cipher_free", None, [vp]),
+    ("rc_encrypted_size", i64, [i64]),
+    ("rc_decrypted_size", i64, [i64, ctypes.POINTER(i32)]),
+    ("rc_calculate_underlying", None, [i64, i64, ctypes.POINTER(i64)]),
+    ("rc_nonce_increment", None, [vp]),
+    ("rc_nonce_add", None, [vp, u64]),
+    ("rc_encrypt_data", vp, [vp, RcReader, ctypes.c_char_p, ctypes.POINTER(i32)]),
+    ("rc_encrypter_read", i64, [vp, vp, i64, ctypes.POINTER(i32)]),
+    ("rc_encrypter_nonce", None, [vp, vp]),
+    ("rc_encrypter_free", None, [vp]),
+    ("rc_decrypt_data", vp, [vp, RcReader, ctypes.POINTER(i32)]),
+    ("rc_decrypt_data_seek", vp, [vp, OPEN_FN, vp, i64, i64, ctypes.POINTER(i32)]),
+    ("rc_decrypter_read", i64, [vp, vp, i64, ctypes.POINTER(i32)]),
+    ("rc_decrypter_range_seek", i64, [vp, i64, i32, i64, ctypes.POINTER(i32)]),
+    ("rc_decrypter_close", i32, [vp]),
+    ("rc_decrypter_nonce", None, [vp, vp]),
+    ("rc_decrypter_wrapped_error", i32, [vp]),
+    ("rc_decrypter_free", None, [vp]),
+    ("rc_error_string", ctypes.c_char_p, [i32]),
+]
+
+SYMBOLS = [s[0] for s in _SIGS]
+
+
+def lib():
+    """Load (building if stale) the native library; raises if it cannot be built/loaded."""
+    global _lib
+    if _lib is None:
+        path = _build.LIB
+        if _build.needs_build():
+            _build.build()
+        if not os.path.exists(path):
+            raise RuntimeError(f"rclone_amd native library missing: {path}")
+        L = ctypes.CDLL(path)
+        for name, res, args in _SIGS:
+            if not hasattr(L, name):
+                continue
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error():
+    return lib().xs_last_error().decode(errors="replace")
+
+
+def check(rc, what="xs call"):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {last_error()}")

@@ -1,0 +1,319 @@
+// xs_api.cpp -- C ABI of the device primitives (include/rclone_crypt_gpu.h, xs_* part).
+//
+// Replaces the per-block secretbox.Seal / secretbox.Open calls of backend/crypt
+// (cipher.go:737, :880) with batched launches: xs_keygen (per-block key schedule) then
+// xs_crypt (one 64 KiB block per workgroup).  The engine keeps per-slot device buffers and
+// streams so host->device copies, kernels and device->host copies of consecutive batches
+// overlap (the host-path number in DESIGN.md).
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "xs_internal.h"
+
+namespace xs {
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+}  // namespace xs
+
+using namespace xs;
+
+static KeyArg key_arg(const uint8_t key[32]) {
+  KeyArg k;
+  for (int i = 0; i < 8; i++) {
+    k.k[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
+             ((uint32_t)key[4 * i + 3] << 24);
+  }
+  return k;
+}
+
+static NonceArg nonce_arg(const uint8_t n[24]) {
+  NonceArg a;
+  for (int i = 0; i < 6; i++) {
+    a.n[i] = (uint32_t)n[4 * i] | ((uint32_t)n[4 * i + 1] << 8) | ((uint32_t)n[4 * i + 2] << 16) |
+             ((uint32_t)n[4 * i + 3] << 24);
+  }
+  return a;
+}
+
+static int hip_fail(hipError_t e, const char* what) {
+  set_error("%s: %s", what, hipGetErrorString(e));
+  return XS_ERR_HIP;
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+extern "C" {
+
+const char* xs_version(void) { return "rclone_amd crypt 0.1 (gfx950)"; }
+
+const char* xs_last_error(void) { return g_err.c_str(); }
+
+int xs_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+size_t xs_workspace_bytes(uint64_t nblocks) { return (size_t)nblocks * sizeof(BlockKey); }
+
+int xs_seal_object_dev(const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block, const void* d_plain,
+                       uint64_t plain_len, void* d_body, void* d_workspace, void* stream) {
+  if (!key || !nonce0 || !d_plain || !d_body || !d_workspace) {
+    set_error("xs_seal_object_dev: null argument");
+    return XS_ERR_INVALID;
+  }
+  if (plain_len == 0) return XS_OK;
+  if (!aligned16(d_plain) || !aligned16(d_body) || !aligned16(d_workspace)) {
+    set_error("xs_seal_object_dev: device buffers must be 16-byte aligned");
+    return XS_ERR_INVALID;
+  }
+  const uint64_t nblocks = (plain_len + XS_BLOCK_DATA - 1) / XS_BLOCK_DATA;
+  hipStream_t s = (hipStream_t)stream;
+  BlockKey* keys = (BlockKey*)d_workspace;
+  hipError_t e = launch_keygen(0, key_arg(key), nonce_arg(nonce0), first_block, plain_len, nblocks, nullptr, keys, s);
+  if (e != hipSuccess) return hip_fail(e, "keygen launch");
+  e = launch_crypt(true, keys, nblocks, (const uint8_t*)d_plain, (uint8_t*)d_body, nullptr, s);
+  if (e != hipSuccess) return hip_fail(e, "seal launch");
+  return XS_OK;
+}
+
+int xs_open_object_dev(const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block, const void* d_body,
+                       uint64_t body_len, void* d_plain, uint8_t* d_ok, void* d_workspace, void* stream) {
+  if (!key || !nonce0 || !d_body || !d_plain || !d_ok || !d_workspace) {
+    set_error("xs_open_object_dev: null argument");
+    return XS_ERR_INVALID;
+  }
+  if (body_len == 0) return XS_OK;
+  if (!aligned16(d_plain) || !aligned16(d_body) || !aligned16(d_workspace)) {
+    set_error("xs_open_object_dev: device buffers must be 16-byte aligned");
+    return XS_ERR_INVALID;
+  }
+  const uint64_t nblocks = (body_len + XS_BLOCK_SIZE - 1) / XS_BLOCK_SIZE;
+  const uint64_t last = body_len - (nblocks - 1) * XS_BLOCK_SIZE;
+  if (last <= XS_BLOCK_HDR) {
+    set_error("xs_open_object_dev: truncated block header (last block %llu bytes)", (unsigned long long)last);
+    return XS_ERR_INVALID;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  BlockKey* keys = (BlockKey*)d_workspace;
+  hipError_t e = launch_keygen(1, key_arg(key), nonce_arg(nonce0), first_block, body_len, nblocks, nullptr, keys, s);
+  if (e != hipSuccess) return hip_fail(e, "keygen launch");
+  e = launch_crypt(false, keys, nblocks, (const uint8_t*)d_body, (uint8_t*)d_plain, d_ok, s);
+  if (e != hipSuccess) return hip_fail(e, "open launch");
+  return XS_OK;
+}
+
+int xs_seal_batch_dev(const uint8_t key[32], const xs_block_desc* d_desc, uint64_t nblocks, const void* d_src,
+                      uint64_t src_len, void* d_dst, uint64_t dst_len, void* d_workspace, void* stream) {
+  if (!key || !d_desc || !d_src || !d_dst || !d_workspace) {
+    set_error("xs_seal_batch_dev: null argument");
+    return XS_ERR_INVALID;
+  }
+  if (nblocks == 0) return XS_OK;
+  NonceArg bounds{};
+  bounds.n[0] = (uint32_t)src_len; bounds.n[1] = (uint32_t)(src_len >> 32);
+  bounds.n[2] = (uint32_t)dst_len; bounds.n[3] = (uint32_t)(dst_len >> 32);
+  bounds.n[4] = (uint32_t)((uintptr_t)d_src & 15u); bounds.n[5] = (uint32_t)((uintptr_t)d_dst & 15u);
+  hipStream_t s = (hipStream_t)stream;
+  BlockKey* keys = (BlockKey*)d_workspace;
+  hipError_t e = launch_keygen(2, key_arg(key), bounds, 0, 0, nblocks, d_desc, keys, s);
+  if (e != hipSuccess) return hip_fail(e, "keygen launch");
+  e = launch_crypt(true, keys, nblocks, (const uint8_t*)d_src, (uint8_t*)d_dst, nullptr, s);
+  if (e != hipSuccess) return hip_fail(e, "seal launch");
+  return XS_OK;
+}
+
+int xs_open_batch_dev(const uint8_t key[32], const xs_block_desc* d_desc, uint64_t nblocks, const void* d_src,
+                      uint64_t src_len, void* d_dst, uint64_t dst_len, uint8_t* d_ok, void* d_workspace,
+                      void* stream) {
+  if (!key || !d_desc || !d_src || !d_dst || !d_ok || !d_workspace) {
+    set_error("xs_open_batch_dev: null argument");
+    return XS_ERR_INVALID;
+  }
+  if (nblocks == 0) return XS_OK;
+  NonceArg bounds{};
+  bounds.n[0] = (uint32_t)src_len; bounds.n[1] = (uint32_t)(src_len >> 32);
+  bounds.n[2] = (uint32_t)dst_len; bounds.n[3] = (uint32_t)(dst_len >> 32);
+  bounds.n[4] = (uint32_t)((uintptr_t)d_src & 15u); bounds.n[5] = (uint32_t)((uintptr_t)d_dst & 15u);
+  hipStream_t s = (hipStream_t)stream;
+  BlockKey* keys = (BlockKey*)d_workspace;
+  hipError_t e = launch_keygen(3, key_arg(key), bounds, 0, 0, nblocks, d_desc, keys, s);
+  if (e != hipSuccess) return hip_fail(e, "keygen launch");
+  e = launch_crypt(false, keys, nblocks, (const uint8_t*)d_src, (uint8_t*)d_dst, d_ok, s);
+  if (e != hipSuccess) return hip_fail(e, "open launch");
+  return XS_OK;
+}
+
+int xs_fill_random_dev(void* d, uint64_t nbytes, uint64_t seed, void* stream) {
+  if (!d || (nbytes & 7u) || !aligned16(d)) {
+    set_error("xs_fill_random_dev: need a 16-byte aligned buffer and a multiple of 8 bytes");
+    return XS_ERR_INVALID;
+  }
+  hipError_t e = launch_fill((uint64_t*)d, nbytes / 8, seed, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "fill launch");
+  return XS_OK;
+}
+
+void* xs_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) {
+    set_error("hipHostMalloc(%zu) failed", bytes);
+    return nullptr;
+  }
+  return p;
+}
+
+void xs_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- engine
+struct xs_engine {
+  int device = 0;
+  uint32_t batch = 0;
+  std::mutex mu;
+  struct Slot {
+    hipStream_t s = nullptr;
+    uint8_t* d_in = nullptr;
+    uint8_t* d_out = nullptr;
+    BlockKey* d_keys = nullptr;
+    uint8_t* d_ok = nullptr;
+  };
+  std::vector<Slot> slots;
+};
+
+static void engine_free(xs_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  for (auto& sl : e->slots) {
+    if (sl.s) (void)hipStreamSynchronize(sl.s);
+    (void)hipFree(sl.d_in);
+    (void)hipFree(sl.d_out);
+    (void)hipFree(sl.d_keys);
+    (void)hipFree(sl.d_ok);
+    if (sl.s) (void)hipStreamDestroy(sl.s);
+  }
+  delete e;
+}
+
+extern "C" xs_engine* xs_engine_create(int device, uint32_t batch_blocks, int nslots) {
+  if (batch_blocks == 0) batch_blocks = 256;
+  if (nslots <= 0) nslots = 3;
+  if (device < 0 || device >= xs_device_count()) {
+    set_error("xs_engine_create: no HIP device %d", device);
+    return nullptr;
+  }
+  xs_engine* e = new xs_engine();
+  e->device = device;
+  e->batch = batch_blocks;
+  if (hipSetDevice(device) != hipSuccess) {
+    set_error("hipSetDevice(%d) failed", device);
+    delete e;
+    return nullptr;
+  }
+  e->slots.resize(nslots);
+  for (auto& sl : e->slots) {
+    const size_t io = (size_t)batch_blocks * XS_BLOCK_SIZE;
+    if (hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&sl.d_in, io) != hipSuccess || hipMalloc(&sl.d_out, io) != hipSuccess ||
+        hipMalloc(&sl.d_keys, (size_t)batch_blocks * sizeof(BlockKey)) != hipSuccess ||
+        hipMalloc(&sl.d_ok, batch_blocks) != hipSuccess) {
+      set_error("xs_engine_create: device allocation failed");
+      engine_free(e);
+      return nullptr;
+    }
+  }
+  return e;
+}
+
+extern "C" void xs_engine_destroy(xs_engine* e) { engine_free(e); }
+
+static int engine_sync(xs_engine* e) {
+  int rc = XS_OK;
+  for (auto& sl : e->slots) {
+    hipError_t err = hipStreamSynchronize(sl.s);
+    if (err != hipSuccess && rc == XS_OK) rc = hip_fail(err, "engine stream");
+  }
+  return rc;
+}
+
+extern "C" int xs_engine_seal(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                              const void* plain, uint64_t plain_len, void* body) {
+  if (!e || !key || !nonce0 || (plain_len && (!plain || !body))) {
+    set_error("xs_engine_seal: null argument");
+    return XS_ERR_INVALID;
+  }
+  std::lock_guard<std::mutex> g(e->mu);
+  if (hipSetDevice(e->device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
+  const KeyArg k = key_arg(key);
+  const NonceArg n = nonce_arg(nonce0);
+  const uint64_t nblocks = (plain_len + XS_BLOCK_DATA - 1) / XS_BLOCK_DATA;
+  for (uint64_t b0 = 0, chunk = 0; b0 < nblocks; b0 += e->batch, chunk++) {
+    auto& sl = e->slots[chunk % e->slots.size()];
+    const uint64_t nb = (nblocks - b0) < e->batch ? (nblocks - b0) : e->batch;
+    const uint64_t in_off = b0 * XS_BLOCK_DATA;
+    const uint64_t in_bytes = (plain_len - in_off) < nb * XS_BLOCK_DATA ? (plain_len - in_off) : nb * XS_BLOCK_DATA;
+    const uint64_t out_bytes = in_bytes + nb * XS_BLOCK_HDR;
+    hipError_t err = hipMemcpyAsync(sl.d_in, (const uint8_t*)plain + in_off, in_bytes, hipMemcpyHostToDevice, sl.s);
+    if (err != hipSuccess) return hip_fail(err, "H2D");
+    err = launch_keygen(0, k, n, first_block + b0, in_bytes, nb, nullptr, sl.d_keys, sl.s);
+    if (err != hipSuccess) return hip_fail(err, "keygen");
+    err = launch_crypt(true, sl.d_keys, nb, sl.d_in, sl.d_out, nullptr, sl.s);
+    if (err != hipSuccess) return hip_fail(err, "seal");
+    err = hipMemcpyAsync((uint8_t*)body + b0 * XS_BLOCK_SIZE, sl.d_out, out_bytes, hipMemcpyDeviceToHost, sl.s);
+    if (err != hipSuccess) return hip_fail(err, "D2H");
+  }
+  return engine_sync(e);
+}
+
+extern "C" int xs_engine_open(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                              const void* body, uint64_t body_len, void* plain, uint8_t* ok) {
+  if (!e || !key || !nonce0 || (body_len && (!body || !plain || !ok))) {
+    set_error("xs_engine_open: null argument");
+    return XS_ERR_INVALID;
+  }
+  if (body_len == 0) return XS_OK;
+  const uint64_t nblocks = (body_len + XS_BLOCK_SIZE - 1) / XS_BLOCK_SIZE;
+  if (body_len - (nblocks - 1) * XS_BLOCK_SIZE <= XS_BLOCK_HDR) {
+    set_error("xs_engine_open: truncated block header");
+    return XS_ERR_INVALID;
+  }
+  std::lock_guard<std::mutex> g(e->mu);
+  if (hipSetDevice(e->device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
+  const KeyArg k = key_arg(key);
+  const NonceArg n = nonce_arg(nonce0);
+  for (uint64_t b0 = 0, chunk = 0; b0 < nblocks; b0 += e->batch, chunk++) {
+    auto& sl = e->slots[chunk % e->slots.size()];
+    const uint64_t nb = (nblocks - b0) < e->batch ? (nblocks - b0) : e->batch;
+    const uint64_t in_off = b0 * XS_BLOCK_SIZE;
+    const uint64_t in_bytes = (body_len - in_off) < nb * XS_BLOCK_SIZE ? (body_len - in_off) : nb * XS_BLOCK_SIZE;
+    const uint64_t out_bytes = in_bytes - nb * XS_BLOCK_HDR;
+    hipError_t err = hipMemcpyAsync(sl.d_in, (const uint8_t*)body + in_off, in_bytes, hipMemcpyHostToDevice, sl.s);
+    if (err != hipSuccess) return hip_fail(err, "H2D");
+    err = launch_keygen(1, k, n, first_block + b0, in_bytes, nb, nullptr, sl.d_keys, sl.s);
+    if (err != hipSuccess) return hip_fail(err, "keygen");
+    err = launch_crypt(false, sl.d_keys, nb, sl.d_in, sl.d_out, sl.d_ok, sl.s);
+    if (err != hipSuccess) return hip_fail(err, "open");
+    err = hipMemcpyAsync((uint8_t*)plain + b0 * XS_BLOCK_DATA, sl.d_out, out_bytes, hipMemcpyDeviceToHost, sl.s);
+    if (err != hipSuccess) return hip_fail(err, "D2H");
+    err = hipMemcpyAsync(ok + b0, sl.d_ok, nb, hipMemcpyDeviceToHost, sl.s);
+    if (err != hipSuccess) return hip_fail(err, "D2H ok");
+  }
+  return engine_sync(e);
+}

@@ -1,0 +1,619 @@
+// xs_kernels.hip -- CDNA4 (gfx950) kernels for rclone's crypt data path.
+//
+// What is computed: NaCl secretbox (XSalsa20 + Poly1305) of every <=64 KiB crypt block,
+// exactly as backend/crypt/cipher.go:737 (secretbox.Seal) and :880 (secretbox.Open) apply
+// it, with block i of an object using nonce0 + i (cipher.go:665-678).
+//
+// Structure (see DESIGN.md "Kernels"):
+//   xs_keygen  one lane per crypt block: per-block nonce, HSalsa20 subkey, keystream
+//              block 0 (Poly1305 key r||s), keystream block 1024 words 0..7 (the last
+//              two 16-byte chunks of a full block) and the Poly1305 power tables the
+//              main kernel needs (r, r^1021, r^0..31, r^(32a)).  ~0.5% of the work.
+//   xs_crypt   one 64 KiB block per 256-lane workgroup (4 wave64s).  Lane t owns the
+//              Salsa20 keystream blocks K = t + 256*s (s = 0..3), i.e. message chunks
+//              4K-2 .. 4K+1 (16 bytes each, offset by the 32-byte Poly1305 key).  A lane
+//              keeps the whole 16-word Salsa20 state in VGPRs; key/nonce words are
+//              wave-uniform and live in SGPRs.  Each lane runs a strided Horner over its
+//              own chunks with uniform multipliers r (inside a group) and r^1021 (between
+//              groups), then multiplies by r^e (e = chunks after its last one) from the
+//              tables; the 256 partial sums are added with wave shuffles + LDS and lane 0
+//              adds s and writes (seal) or checks (open) the tag.
+//   Poly1305 arithmetic is radix 2^26 (5 limbs): the product columns are
+//   v_mad_u64_u32 chains, which measured as fast as v_alignbit on gfx950.
+//
+// There is no MFMA here: the work is 32-bit add/rotate/xor (Salsa20) and 32x32->64
+// multiply-add (Poly1305) on the VALU, plus one HBM read and one HBM write per byte.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "xs_internal.h"
+
+namespace xs {
+
+constexpr uint32_t M26 = 0x3ffffffu;
+
+struct P5 {
+  uint32_t v[5];
+};
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) {
+  return __builtin_amdgcn_alignbit(x, x, 32 - n);
+}
+
+__device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, int s) {
+  return __builtin_amdgcn_alignbit(hi, lo, s);
+}
+
+#define XS_QR(a, b, c, d)        \
+  b ^= rotl(a + d, 7);           \
+  c ^= rotl(b + a, 9);           \
+  d ^= rotl(c + b, 13);          \
+  a ^= rotl(d + c, 18);
+
+__device__ __forceinline__ void salsa_rounds(uint32_t (&x)[16]) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    XS_QR(x[0], x[4], x[8], x[12]);
+    XS_QR(x[5], x[9], x[13], x[1]);
+    XS_QR(x[10], x[14], x[2], x[6]);
+    XS_QR(x[15], x[3], x[7], x[11]);
+    XS_QR(x[0], x[1], x[2], x[3]);
+    XS_QR(x[5], x[6], x[7], x[4]);
+    XS_QR(x[10], x[11], x[8], x[9]);
+    XS_QR(x[15], x[12], x[13], x[14]);
+  }
+}
+
+constexpr uint32_t SIG0 = 0x61707865u, SIG1 = 0x3320646eu, SIG2 = 0x79622d32u, SIG3 = 0x6b206574u;
+
+// Salsa20/20 keystream block `ctr` for a 32-byte key (k[8]) and 8-byte nonce (n0, n1).
+__device__ __forceinline__ void salsa20_block(const uint32_t (&k)[8], uint32_t n0, uint32_t n1,
+                                              uint32_t ctr, uint32_t (&out)[16]) {
+  uint32_t x[16] = {SIG0, k[0], k[1], k[2], k[3], SIG1, n0, n1,
+                    ctr,  0u,   SIG2, k[4], k[5], k[6], k[7], SIG3};
+  salsa_rounds(x);
+  out[0] = x[0] + SIG0;
+  out[1] = x[1] + k[0];
+  out[2] = x[2] + k[1];
+  out[3] = x[3] + k[2];
+  out[4] = x[4] + k[3];
+  out[5] = x[5] + SIG1;
+  out[6] = x[6] + n0;
+  out[7] = x[7] + n1;
+  out[8] = x[8] + ctr;
+  out[9] = x[9];
+  out[10] = x[10] + SIG2;
+  out[11] = x[11] + k[4];
+  out[12] = x[12] + k[5];
+  out[13] = x[13] + k[6];
+  out[14] = x[14] + k[7];
+  out[15] = x[15] + SIG3;
+}
+
+// ---------------------------------------------------------------- Poly1305, radix 2^26
+// h * m mod 2^130-5.  Limbs of h < 2^27, limbs of m < 2^26 + 2^6 (bounds keep every
+// column sum < 2^58 and every carry*5 < 2^32).  Carries are folded into the next column's
+// mad chain.
+__device__ __forceinline__ P5 pmul(const P5& h, const P5& m) {
+  const uint32_t s1 = m.v[1] * 5, s2 = m.v[2] * 5, s3 = m.v[3] * 5, s4 = m.v[4] * 5;
+  uint64_t d0 = (uint64_t)h.v[0] * m.v[0] + (uint64_t)h.v[1] * s4 + (uint64_t)h.v[2] * s3 +
+                (uint64_t)h.v[3] * s2 + (uint64_t)h.v[4] * s1;
+  P5 o;
+  o.v[0] = (uint32_t)d0 & M26;
+  uint64_t d1 = (d0 >> 26) + (uint64_t)h.v[0] * m.v[1] + (uint64_t)h.v[1] * m.v[0] +
+                (uint64_t)h.v[2] * s4 + (uint64_t)h.v[3] * s3 + (uint64_t)h.v[4] * s2;
+  o.v[1] = (uint32_t)d1 & M26;
+  uint64_t d2 = (d1 >> 26) + (uint64_t)h.v[0] * m.v[2] + (uint64_t)h.v[1] * m.v[1] +
+                (uint64_t)h.v[2] * m.v[0] + (uint64_t)h.v[3] * s4 + (uint64_t)h.v[4] * s3;
+  o.v[2] = (uint32_t)d2 & M26;
+  uint64_t d3 = (d2 >> 26) + (uint64_t)h.v[0] * m.v[3] + (uint64_t)h.v[1] * m.v[2] +
+                (uint64_t)h.v[2] * m.v[1] + (uint64_t)h.v[3] * m.v[0] + (uint64_t)h.v[4] * s4;
+  o.v[3] = (uint32_t)d3 & M26;
+  uint64_t d4 = (d3 >> 26) + (uint64_t)h.v[0] * m.v[4] + (uint64_t)h.v[1] * m.v[3] +
+                (uint64_t)h.v[2] * m.v[2] + (uint64_t)h.v[3] * m.v[1] + (uint64_t)h.v[4] * m.v[0];
+  o.v[4] = (uint32_t)d4 & M26;
+  uint32_t c = (uint32_t)(d4 >> 26);
+  o.v[0] += c * 5;
+  c = o.v[0] >> 26;
+  o.v[0] &= M26;
+  o.v[1] += c;
+  return o;
+}
+
+// Same product when the multiplier is wave-uniform and its 5*m limbs are precomputed.
+struct PMul {
+  uint32_t m[5], s[5];
+};
+
+__device__ __forceinline__ PMul pmul_prep(const P5& m) {
+  PMul p;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    p.m[i] = m.v[i];
+    p.s[i] = m.v[i] * 5;
+  }
+  return p;
+}
+
+__device__ __forceinline__ P5 pmul_u(const P5& h, const PMul& M) {
+  uint64_t d0 = (uint64_t)h.v[0] * M.m[0] + (uint64_t)h.v[1] * M.s[4] + (uint64_t)h.v[2] * M.s[3] +
+                (uint64_t)h.v[3] * M.s[2] + (uint64_t)h.v[4] * M.s[1];
+  P5 o;
+  o.v[0] = (uint32_t)d0 & M26;
+  uint64_t d1 = (d0 >> 26) + (uint64_t)h.v[0] * M.m[1] + (uint64_t)h.v[1] * M.m[0] +
+                (uint64_t)h.v[2] * M.s[4] + (uint64_t)h.v[3] * M.s[3] + (uint64_t)h.v[4] * M.s[2];
+  o.v[1] = (uint32_t)d1 & M26;
+  uint64_t d2 = (d1 >> 26) + (uint64_t)h.v[0] * M.m[2] + (uint64_t)h.v[1] * M.m[1] +
+                (uint64_t)h.v[2] * M.m[0] + (uint64_t)h.v[3] * M.s[4] + (uint64_t)h.v[4] * M.s[3];
+  o.v[2] = (uint32_t)d2 & M26;
+  uint64_t d3 = (d2 >> 26) + (uint64_t)h.v[0] * M.m[3] + (uint64_t)h.v[1] * M.m[2] +
+                (uint64_t)h.v[2] * M.m[1] + (uint64_t)h.v[3] * M.m[0] + (uint64_t)h.v[4] * M.s[4];
+  o.v[3] = (uint32_t)d3 & M26;
+  uint64_t d4 = (d3 >> 26) + (uint64_t)h.v[0] * M.m[4] + (uint64_t)h.v[1] * M.m[3] +
+                (uint64_t)h.v[2] * M.m[2] + (uint64_t)h.v[3] * M.m[1] + (uint64_t)h.v[4] * M.m[0];
+  o.v[4] = (uint32_t)d4 & M26;
+  uint32_t c = (uint32_t)(d4 >> 26);
+  o.v[0] += c * 5;
+  c = o.v[0] >> 26;
+  o.v[0] &= M26;
+  o.v[1] += c;
+  return o;
+}
+
+// h += 16-byte chunk (LE words w0..w3) with the 2^128 pad bit (full chunks).
+__device__ __forceinline__ void padd_full(P5& h, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  h.v[0] += w0 & M26;
+  h.v[1] += alignbit(w1, w0, 26) & M26;
+  h.v[2] += alignbit(w2, w1, 20) & M26;
+  h.v[3] += alignbit(w3, w2, 14) & M26;
+  h.v[4] += (w3 >> 8) | (1u << 24);
+}
+
+// h += partial chunk already padded with 0x01 at byte L (no 2^128 bit).
+__device__ __forceinline__ void padd_part(P5& h, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  h.v[0] += w0 & M26;
+  h.v[1] += alignbit(w1, w0, 26) & M26;
+  h.v[2] += alignbit(w2, w1, 20) & M26;
+  h.v[3] += alignbit(w3, w2, 14) & M26;
+  h.v[4] += (w3 >> 8);
+}
+
+// Carry-normalise limbs < 2^32 into limbs < 2^26 (+2^6 on limb 1), value mod p preserved.
+__device__ __forceinline__ void pnorm(P5& h) {
+  uint32_t c;
+  c = h.v[0] >> 26; h.v[0] &= M26; h.v[1] += c;
+  c = h.v[1] >> 26; h.v[1] &= M26; h.v[2] += c;
+  c = h.v[2] >> 26; h.v[2] &= M26; h.v[3] += c;
+  c = h.v[3] >> 26; h.v[3] &= M26; h.v[4] += c;
+  c = h.v[4] >> 26; h.v[4] &= M26; h.v[0] += c * 5;
+  c = h.v[0] >> 26; h.v[0] &= M26; h.v[1] += c;
+}
+
+// Fully reduce mod p = 2^130-5 (canonical limbs).
+__device__ __forceinline__ P5 pcanon(P5 h) {
+  pnorm(h);
+  pnorm(h);
+  uint32_t c;
+  c = h.v[1] >> 26; h.v[1] &= M26; h.v[2] += c;
+  c = h.v[2] >> 26; h.v[2] &= M26; h.v[3] += c;
+  c = h.v[3] >> 26; h.v[3] &= M26; h.v[4] += c;
+  c = h.v[4] >> 26; h.v[4] &= M26; h.v[0] += c * 5;
+  c = h.v[0] >> 26; h.v[0] &= M26; h.v[1] += c;
+  uint32_t g0 = h.v[0] + 5; c = g0 >> 26; g0 &= M26;
+  uint32_t g1 = h.v[1] + c; c = g1 >> 26; g1 &= M26;
+  uint32_t g2 = h.v[2] + c; c = g2 >> 26; g2 &= M26;
+  uint32_t g3 = h.v[3] + c; c = g3 >> 26; g3 &= M26;
+  uint32_t g4 = h.v[4] + c - (1u << 26);
+  uint32_t mask = (g4 >> 31) - 1u;
+  P5 o;
+  o.v[0] = (h.v[0] & ~mask) | (g0 & mask);
+  o.v[1] = (h.v[1] & ~mask) | (g1 & mask);
+  o.v[2] = (h.v[2] & ~mask) | (g2 & mask);
+  o.v[3] = (h.v[3] & ~mask) | (g3 & mask);
+  o.v[4] = (h.v[4] & ~mask) | (g4 & mask);
+  return o;
+}
+
+__device__ __forceinline__ void ptag(const P5& hc, const uint32_t (&s)[4], uint32_t (&tag)[4]) {
+  const uint32_t w0 = hc.v[0] | (hc.v[1] << 26), w1 = (hc.v[1] >> 6) | (hc.v[2] << 20),
+                 w2 = (hc.v[2] >> 12) | (hc.v[3] << 14), w3 = (hc.v[3] >> 18) | (hc.v[4] << 8);
+  uint64_t f = (uint64_t)w0 + s[0];
+  tag[0] = (uint32_t)f;
+  f = (uint64_t)w1 + s[1] + (f >> 32);
+  tag[1] = (uint32_t)f;
+  f = (uint64_t)w2 + s[2] + (f >> 32);
+  tag[2] = (uint32_t)f;
+  f = (uint64_t)w3 + s[3] + (f >> 32);
+  tag[3] = (uint32_t)f;
+}
+
+// ---------------------------------------------------------------- keygen
+// One lane per crypt block.  MODE: 0 object seal, 1 object open, 2 descriptor seal,
+// 3 descriptor open.  Object mode derives nonce, offsets and length from the block
+// index (cipher.go:665-678 nonce.add; :1121 EncryptedSize layout).
+template <int MODE>
+__global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uint64_t first_block,
+                                                uint64_t total_len, uint64_t nblocks,
+                                                const xs_block_desc* __restrict__ desc,
+                                                BlockKey* __restrict__ out) {
+  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  uint32_t n[6];
+  uint64_t src, dst;
+  uint32_t len;
+  if constexpr (MODE < 2) {
+    // 192-bit little-endian nonce0 + (first_block + b) == nonce.add (cipher.go:665)
+    uint64_t add = first_block + b;
+    uint64_t lo = ((uint64_t)nonce0.n[1] << 32) | nonce0.n[0];
+    uint64_t sum = lo + add;
+    uint32_t carry = sum < lo ? 1u : 0u;
+    n[0] = (uint32_t)sum;
+    n[1] = (uint32_t)(sum >> 32);
+#pragma unroll
+    for (int i = 2; i < 6; i++) {
+      uint32_t v = nonce0.n[i] + carry;
+      carry = (carry && v == 0) ? 1u : 0u;
+      n[i] = v;
+    }
+    if constexpr (MODE == 0) {
+      src = b * XS_BLOCK_DATA;
+      dst = b * XS_BLOCK_SIZE;
+      uint64_t rem = total_len - src;
+      len = (uint32_t)(rem < XS_BLOCK_DATA ? rem : XS_BLOCK_DATA);
+    } else {
+      src = b * XS_BLOCK_SIZE;
+      dst = b * XS_BLOCK_DATA;
+      uint64_t rem = total_len - src;
+      len = (uint32_t)(rem < XS_BLOCK_SIZE ? rem : XS_BLOCK_SIZE) - XS_BLOCK_HDR;
+    }
+  } else {
+    const xs_block_desc& d = desc[b];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      n[i] = (uint32_t)d.nonce[4 * i] | ((uint32_t)d.nonce[4 * i + 1] << 8) |
+             ((uint32_t)d.nonce[4 * i + 2] << 16) | ((uint32_t)d.nonce[4 * i + 3] << 24);
+    }
+    src = d.src_off;
+    dst = d.dst_off;
+    len = d.len;
+    // descriptor validation (bounds + 16-byte payload alignment); nonce0 carries
+    // {src_len, dst_len, src base misalignment, dst base misalignment}
+    const uint64_t src_len = ((uint64_t)nonce0.n[1] << 32) | nonce0.n[0];
+    const uint64_t dst_len = ((uint64_t)nonce0.n[3] << 32) | nonce0.n[2];
+    const uint64_t in_need = (uint64_t)len + (MODE == 3 ? XS_BLOCK_HDR : 0u);
+    const uint64_t out_need = (uint64_t)len + (MODE == 2 ? XS_BLOCK_HDR : 0u);
+    const uint64_t in_pay = src + (MODE == 3 ? XS_BLOCK_HDR : 0u) + nonce0.n[4];
+    const uint64_t out_pay = dst + (MODE == 2 ? XS_BLOCK_HDR : 0u) + nonce0.n[5];
+    const bool bad = len == 0 || len > XS_BLOCK_DATA || src > src_len || in_need > src_len - src ||
+                     dst > dst_len || out_need > dst_len - dst || (in_pay & 15u) || (out_pay & 15u);
+    if (bad) {
+      out[b].flags = 1;
+      out[b].len = 0;
+      return;
+    }
+  }
+  // HSalsa20(key, nonce[0:16]) -> subkey
+  uint32_t x[16] = {SIG0, key.k[0], key.k[1], key.k[2], key.k[3], SIG1, n[0], n[1],
+                    n[2], n[3],     SIG2,     key.k[4], key.k[5], key.k[6], key.k[7], SIG3};
+  salsa_rounds(x);
+  uint32_t sk[8] = {x[0], x[5], x[10], x[15], x[6], x[7], x[8], x[9]};
+  uint32_t ks[16];
+  salsa20_block(sk, n[4], n[5], 0u, ks);
+  BlockKey* o = out + b;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o->subkey[i] = sk[i];
+  o->n2[0] = n[4];
+  o->n2[1] = n[5];
+  o->len = len;
+  o->flags = 0;
+  o->src = src;
+  o->dst = dst;
+#pragma unroll
+  for (int i = 0; i < 4; i++) o->s[i] = ks[4 + i];
+  // clamp r (bytes 0..15 of keystream block 0) into radix-2^26 limbs
+  P5 r;
+  r.v[0] = ks[0] & 0x3ffffffu;
+  r.v[1] = alignbit(ks[1], ks[0], 26) & 0x3ffff03u;
+  r.v[2] = alignbit(ks[2], ks[1], 20) & 0x3ffc0ffu;
+  r.v[3] = alignbit(ks[3], ks[2], 14) & 0x3f03fffu;
+  r.v[4] = (ks[3] >> 8) & 0x00fffffu;
+  if (len > XS_BLOCK_DATA - 32) {
+    uint32_t ks2[16];
+    salsa20_block(sk, n[4], n[5], 1024u, ks2);
+#pragma unroll
+    for (int i = 0; i < 8; i++) o->ks1024[i] = ks2[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 5; i++) o->r[i] = r.v[i];
+  P5 p;
+  p.v[0] = 1; p.v[1] = 0; p.v[2] = 0; p.v[3] = 0; p.v[4] = 0;
+  for (int i = 0; i < 32; i++) {
+#pragma unroll
+    for (int j = 0; j < 5; j++) o->T1[i][j] = p.v[j];
+    if (i < 31) p = pcanon(pmul(p, r));
+  }
+  P5 r31 = p;
+  P5 r32 = pcanon(pmul(p, r));
+  p.v[0] = 1; p.v[1] = 0; p.v[2] = 0; p.v[3] = 0; p.v[4] = 0;
+  for (int a = 0; a < 32; a++) {
+#pragma unroll
+    for (int j = 0; j < 5; j++) o->T2[a][j] = p.v[j];
+    if (a < 31) p = pcanon(pmul(p, r32));
+  }
+  // r^1021 = r^992 * r^29
+  P5 r29;
+#pragma unroll
+  for (int j = 0; j < 5; j++) r29.v[j] = o->T1[29][j];
+  (void)r31;
+  P5 R = pcanon(pmul(p, r29));
+#pragma unroll
+  for (int i = 0; i < 5; i++) o->R[i] = R.v[i];
+}
+
+// ---------------------------------------------------------------- main block kernel
+// SEAL: in = plaintext block, out = tag(16) || ct.   OPEN: in = tag || ct, out = plaintext,
+// ok[blk] = 1 if the tag verified (else the plaintext is zero-filled, the
+// pass_bad_blocks contract of cipher.go:885-893).
+template <bool SEAL>
+__global__ void __launch_bounds__(256) xs_crypt(const BlockKey* __restrict__ keys, const uint8_t* __restrict__ src,
+                                                uint8_t* __restrict__ dst, uint8_t* __restrict__ ok) {
+  __shared__ uint32_t red[4][5];
+  __shared__ uint32_t verdict;
+  const BlockKey* bk = keys + blockIdx.x;
+  if (bk->flags) {  // rejected descriptor: write nothing
+    if (!SEAL && threadIdx.x == 0) ok[blockIdx.x] = 0;
+    return;
+  }
+  const uint32_t n = bk->len;
+  const uint8_t* in = src + bk->src;
+  uint8_t* out = dst + bk->dst;
+  const uint8_t* pin = SEAL ? in : in + XS_BLOCK_HDR;
+  uint8_t* pout = SEAL ? out + XS_BLOCK_HDR : out;
+  const uint32_t t = threadIdx.x;
+  const int nc = (int)((n + 15u) >> 4);
+
+  uint32_t k[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) k[i] = bk->subkey[i];
+  const uint32_t n0 = bk->n2[0], n1 = bk->n2[1];
+  P5 rr, RR;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    rr.v[i] = bk->r[i];
+    RR.v[i] = bk->R[i];
+  }
+  const PMul Mr = pmul_prep(rr), MR = pmul_prep(RR);
+
+  P5 h;
+  h.v[0] = h.v[1] = h.v[2] = h.v[3] = h.v[4] = 0;
+  int c_last = -1;
+
+#pragma unroll 1
+  for (int s = 0; s < 4; s++) {
+    const uint32_t K = t + 256u * (uint32_t)s;
+    const int cfirst = 4 * (int)K - 2;
+    if (cfirst >= nc) break;
+    const bool has_next = (cfirst + 1024) < nc;
+    const bool fast = (K > 0) && (64u * K + 32u <= n);
+    uint32_t d[16];
+    if (fast) {
+      const uint4* p = reinterpret_cast<const uint4*>(pin + 64u * K - 32u);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        uint4 v = p[j];
+        d[4 * j] = v.x; d[4 * j + 1] = v.y; d[4 * j + 2] = v.z; d[4 * j + 3] = v.w;
+      }
+    }
+    uint32_t ks[16];
+    salsa20_block(k, n0, n1, K, ks);
+    if (fast) {
+      uint32_t o[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) o[i] = d[i] ^ ks[i];
+      uint4* q = reinterpret_cast<uint4*>(pout + 64u * K - 32u);
+#pragma unroll
+      for (int j = 0; j < 4; j++) q[j] = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
+      const uint32_t* c = SEAL ? o : d;  // Poly1305 runs over the ciphertext
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        padd_full(h, c[4 * j], c[4 * j + 1], c[4 * j + 2], c[4 * j + 3]);
+        h = pmul_u(h, Mr);
+      }
+      padd_full(h, c[12], c[13], c[14], c[15]);
+      {
+        PMul M3;
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          M3.m[i] = has_next ? MR.m[i] : Mr.m[i];
+          M3.s[i] = has_next ? MR.s[i] : Mr.s[i];
+        }
+        h = pmul_u(h, M3);
+      }
+      c_last = cfirst + 3;
+    } else {
+      // boundary group: K == 0 (first two chunks are the Poly1305 key) or the block tail
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int c = cfirst + j;
+        if (c < 0 || c >= nc) continue;
+        const uint32_t off = 16u * (uint32_t)c;
+        const uint32_t L = (n - off) < 16u ? (n - off) : 16u;
+        uint32_t w[4];
+        if (L == 16u) {
+          uint4 v = *reinterpret_cast<const uint4*>(pin + off);
+          w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else {
+          uint8_t bb[16];
+#pragma unroll
+          for (int i = 0; i < 16; i++) bb[i] = (uint32_t)i < L ? pin[off + i] : 0;
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            w[i] = (uint32_t)bb[4 * i] | ((uint32_t)bb[4 * i + 1] << 8) | ((uint32_t)bb[4 * i + 2] << 16) |
+                   ((uint32_t)bb[4 * i + 3] << 24);
+        }
+        uint32_t o4[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) o4[i] = w[i] ^ ks[4 * j + i];
+        if (L < 16u) {
+          // keep only the first L bytes of the output chunk
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int lo = 4 * i;
+            uint32_t keep = (L >= (uint32_t)lo + 4u) ? 0xffffffffu
+                            : (L <= (uint32_t)lo ? 0u : ((1u << (8u * (L - (uint32_t)lo))) - 1u));
+            o4[i] &= keep;
+            w[i] &= keep;
+          }
+        }
+        if (L == 16u) {
+          *reinterpret_cast<uint4*>(pout + off) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+        } else {
+          for (uint32_t i = 0; i < L; i++) pout[off + i] = (uint8_t)(o4[i >> 2] >> (8u * (i & 3u)));
+        }
+        uint32_t cw[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) cw[i] = SEAL ? o4[i] : w[i];
+        if (L == 16u) {
+          padd_full(h, cw[0], cw[1], cw[2], cw[3]);
+        } else {
+          // pad byte 0x01 at position L
+          cw[L >> 2] |= 1u << (8u * (L & 3u));
+          padd_part(h, cw[0], cw[1], cw[2], cw[3]);
+        }
+        if (j == 3 && has_next) h = pmul_u(h, MR);
+        else h = pmul_u(h, Mr);
+        c_last = c;
+      }
+    }
+  }
+  // lane 0 also owns chunks 4094, 4095 (keystream block 1024, precomputed by keygen)
+  if (t == 0 && nc > 4094) {
+#pragma unroll 1
+    for (int j = 0; j < 2; j++) {
+      const int c = 4094 + j;
+      if (c >= nc) break;
+      const uint32_t off = 16u * (uint32_t)c;
+      const uint32_t L = (n - off) < 16u ? (n - off) : 16u;
+      uint32_t w[4], o4[4];
+      for (int i = 0; i < 4; i++) {
+        uint32_t v = 0;
+        for (int bI = 0; bI < 4; bI++) {
+          uint32_t pos = 4u * i + bI;
+          if (pos < L) v |= (uint32_t)pin[off + pos] << (8 * bI);
+        }
+        w[i] = v;
+        uint32_t keep = (L >= 4u * i + 4u) ? 0xffffffffu : (L <= 4u * i ? 0u : ((1u << (8u * (L - 4u * i))) - 1u));
+        o4[i] = (v ^ bk->ks1024[4 * j + i]) & keep;
+      }
+      for (uint32_t i = 0; i < L; i++) pout[off + i] = (uint8_t)(o4[i >> 2] >> (8u * (i & 3u)));
+      uint32_t cw[4];
+      for (int i = 0; i < 4; i++) cw[i] = SEAL ? o4[i] : w[i];
+      if (L == 16u) {
+        padd_full(h, cw[0], cw[1], cw[2], cw[3]);
+      } else {
+        cw[L >> 2] |= 1u << (8u * (L & 3u));
+        padd_part(h, cw[0], cw[1], cw[2], cw[3]);
+      }
+      h = pmul_u(h, Mr);
+      c_last = c;
+    }
+  }
+  // bring every lane's partial to exponent 0: multiply by r^(nc-1-c_last)
+  if (c_last >= 0) {
+    const uint32_t e = (uint32_t)(nc - 1 - c_last);
+    P5 t1, t2;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      t1.v[i] = bk->T1[e & 31u][i];
+      t2.v[i] = bk->T2[e >> 5][i];
+    }
+    h = pmul(h, pmul(t1, t2));
+  }
+  // sum the 256 partials: wave shuffles, then LDS across the 4 waves
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+    for (int i = 0; i < 5; i++) h.v[i] += (uint32_t)__shfl_xor((int)h.v[i], off, 64);
+    if (off == 2) pnorm(h);
+  }
+  const uint32_t wave = t >> 6, lane = t & 63u;
+  if (!SEAL) __builtin_amdgcn_s_waitcnt(0);  // our plaintext stores complete before a possible zero-fill
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 5; i++) red[wave][i] = h.v[i];
+  }
+  __syncthreads();
+  if (t == 0) {
+    P5 acc;
+#pragma unroll
+    for (int i = 0; i < 5; i++) acc.v[i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    P5 hc = pcanon(acc);
+    uint32_t s4[4] = {bk->s[0], bk->s[1], bk->s[2], bk->s[3]};
+    uint32_t tag[4];
+    ptag(hc, s4, tag);
+    if (SEAL) {
+      *reinterpret_cast<uint4*>(out) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+    } else {
+      uint4 want = *reinterpret_cast<const uint4*>(in);
+      uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) | (want.z ^ tag[2]) | (want.w ^ tag[3]);
+      verdict = diff == 0 ? 1u : 0u;
+      ok[blockIdx.x] = diff == 0 ? 1 : 0;
+    }
+  }
+  if (!SEAL) {
+    __syncthreads();
+    if (verdict == 0) {
+      // authentication failed: zero the block's plaintext (ordered after the stores above)
+      for (uint32_t off = 16u * t; off < n; off += 16u * 256u) {
+        const uint32_t L = (n - off) < 16u ? (n - off) : 16u;
+        if (L == 16u) *reinterpret_cast<uint4*>(pout + off) = make_uint4(0, 0, 0, 0);
+        else for (uint32_t i = 0; i < L; i++) pout[off + i] = 0;
+      }
+    }
+  }
+}
+
+// SplitMix64 fill (synthetic benchmark objects generated in HBM): word k = mix(seed + (k+1)*golden)
+__global__ void xs_fill_splitmix(uint64_t* __restrict__ dst, uint64_t nwords, uint64_t seed) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nwords;
+       k += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t z = seed + (k + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    dst[k] = z ^ (z >> 31);
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+hipError_t launch_keygen(int mode, const KeyArg& key, const NonceArg& nonce0, uint64_t first_block,
+                         uint64_t total_len, uint64_t nblocks, const xs_block_desc* desc, BlockKey* out,
+                         hipStream_t stream) {
+  if (nblocks == 0) return hipSuccess;
+  const uint64_t grid = (nblocks + 63) / 64;
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(xs_keygen<0>, dim3((unsigned)grid), dim3(64), 0, stream, key, nonce0, first_block, total_len, nblocks, desc, out); break;
+    case 1: hipLaunchKernelGGL(xs_keygen<1>, dim3((unsigned)grid), dim3(64), 0, stream, key, nonce0, first_block, total_len, nblocks, desc, out); break;
+    case 2: hipLaunchKernelGGL(xs_keygen<2>, dim3((unsigned)grid), dim3(64), 0, stream, key, nonce0, first_block, total_len, nblocks, desc, out); break;
+    default: hipLaunchKernelGGL(xs_keygen<3>, dim3((unsigned)grid), dim3(64), 0, stream, key, nonce0, first_block, total_len, nblocks, desc, out); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const uint8_t* src, uint8_t* dst,
+                        uint8_t* ok, hipStream_t stream) {
+  if (nblocks == 0) return hipSuccess;
+  if (seal) hipLaunchKernelGGL(xs_crypt<true>, dim3((unsigned)nblocks), dim3(256), 0, stream, keys, src, dst, ok);
+  else hipLaunchKernelGGL(xs_crypt<false>, dim3((unsigned)nblocks), dim3(256), 0, stream, keys, src, dst, ok);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, hipStream_t stream) {
+  if (nwords == 0) return hipSuccess;
+  uint64_t grid = (nwords + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(xs_fill_splitmix, dim3((unsigned)grid), dim3(256), 0, stream, dst, nwords, seed);
+  return hipGetLastError();
+}
+
+}  // namespace xs

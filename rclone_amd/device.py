@@ -1,0 +1,97 @@
+"""Device-resident entry points (torch tensors as HBM buffers; torch is plumbing only).
+
+Thin wrappers over the xs_*_dev C ABI: the compute runs in the HIP kernels of
+librclone_crypt.so on the tensors' device and on torch's current stream of that device.
+"""
+import torch
+
+from . import _lib
+
+BLOCK_DATA = 65536
+BLOCK_HDR = 16
+BLOCK_SIZE = 65552
+FILE_HDR = 32
+
+
+def _stream(t):
+    return ctypes_void(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def ctypes_void(x):
+    import ctypes
+    return ctypes.c_void_p(x)
+
+
+def _require_gpu(*ts):
+    for t in ts:
+        if not t.is_cuda:
+            raise ValueError("rclone_amd.device needs HIP device tensors (no CPU fallback)")
+        if not t.is_contiguous():
+            raise ValueError("tensors must be contiguous")
+
+
+def body_size(plain_len: int) -> int:
+    """Bytes of wire blocks (EncryptedSize minus the 32-byte file header)."""
+    full, rem = divmod(plain_len, BLOCK_DATA)
+    return full * BLOCK_SIZE + (rem + BLOCK_HDR if rem else 0)
+
+
+def plain_size(body_len: int) -> int:
+    full, rem = divmod(body_len, BLOCK_SIZE)
+    if rem and rem <= BLOCK_HDR:
+        raise ValueError("truncated block header")
+    return full * BLOCK_DATA + (rem - BLOCK_HDR if rem else 0)
+
+
+def nblocks_plain(plain_len: int) -> int:
+    return (plain_len + BLOCK_DATA - 1) // BLOCK_DATA
+
+
+def workspace(nblocks: int, device) -> torch.Tensor:
+    nbytes = _lib.lib().xs_workspace_bytes(nblocks)
+    return torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
+
+
+def seal_object(key: bytes, nonce0: bytes, plain: torch.Tensor, body: torch.Tensor = None,
+                first_block: int = 0, ws: torch.Tensor = None) -> torch.Tensor:
+    """Seal a plaintext object (uint8 tensor in HBM) into wire blocks (no 32-byte header)."""
+    _require_gpu(plain)
+    n = plain.numel()
+    if body is None:
+        body = torch.empty(body_size(n), dtype=torch.uint8, device=plain.device)
+    if ws is None:
+        ws = workspace(nblocks_plain(n), plain.device)
+    _require_gpu(body, ws)
+    assert body.numel() >= body_size(n) and ws.numel() >= _lib.lib().xs_workspace_bytes(nblocks_plain(n))
+    rc = _lib.lib().xs_seal_object_dev(bytes(key), bytes(nonce0), first_block, plain.data_ptr(), n,
+                                       body.data_ptr(), ws.data_ptr(), _stream(plain))
+    _lib.check(rc, "xs_seal_object_dev")
+    return body
+
+
+def open_object(key: bytes, nonce0: bytes, body: torch.Tensor, plain: torch.Tensor = None,
+                ok: torch.Tensor = None, first_block: int = 0, ws: torch.Tensor = None):
+    """Open wire blocks; returns (plaintext tensor, ok uint8 tensor per block)."""
+    _require_gpu(body)
+    m = body.numel()
+    n = plain_size(m)
+    nb = (m + BLOCK_SIZE - 1) // BLOCK_SIZE
+    if plain is None:
+        plain = torch.empty(max(n, 16), dtype=torch.uint8, device=body.device)
+    if ok is None:
+        ok = torch.empty(max(nb, 1), dtype=torch.uint8, device=body.device)
+    if ws is None:
+        ws = workspace(nb, body.device)
+    _require_gpu(plain, ok, ws)
+    assert plain.numel() >= n and ok.numel() >= nb and ws.numel() >= _lib.lib().xs_workspace_bytes(nb)
+    rc = _lib.lib().xs_open_object_dev(bytes(key), bytes(nonce0), first_block, body.data_ptr(), m,
+                                       plain.data_ptr(), ok.data_ptr(), ws.data_ptr(), _stream(body))
+    _lib.check(rc, "xs_open_object_dev")
+    return plain[:n], ok[:nb]
+
+
+def fill_random(t: torch.Tensor, seed: int):
+    _require_gpu(t)
+    rc = _lib.lib().xs_fill_random_dev(t.data_ptr(), t.numel() * t.element_size(), seed, _stream(t))
+    _lib.check(rc, "xs_fill_random_dev")
+    return t
