@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident crypt block encrypt+decrypt on MI355X (BASELINE.json metric).
+
+One step = seal (encrypt) every 64 KiB block of a resident 100k-block object set, then
+open (decrypt + verify) all of them: keygen + block kernel per direction, inputs already in
+HBM (BASELINE.json configs[1] "1xMI355X encrypt: 100k x 64KiB device-resident blocks", with
+the decrypt pass of configs[2] on the same blocks).  value = plaintext GiB pushed through the
+cipher per second, both directions counted (2 x 6.25 GiB per step per GPU), summed over
+ranks (weak scaling: every rank owns its own 100k blocks = its round-robin share of a larger
+object set; no payload crosses ranks).  Counters (blocks, bytes, tag failures) are summed
+across ranks with one RCCL all-reduce after the timed region.
+
+Also reported: the dominant kernel's roofline (HBM; achieved algorithmic GB/s from HIP events
+around every xs_crypt launch inside the timed region) and the CPU baseline (the oracle's
+C restatement, OpenMP, on this host's cores, bounded sample) -- see DESIGN.md.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--blocks B] [--no-cpu]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "device-resident GiB/s, 64KiB-block crypt encrypt+decrypt, 1/2/4/8 MI355X"
+BLOCK_DATA = 65536
+BLOCK_SIZE = 65552
+# algorithmic HBM bytes per 64 KiB block per launch:
+#   seal: read 65536 plaintext + write 65552 wire block + 1440 key schedule read
+#   open: read 65552 wire block + write 65536 plaintext + 1 ok byte + 1440 key schedule read
+ALG_BYTES_SEAL = 65536 + 65552 + 1440
+ALG_BYTES_OPEN = 65552 + 65536 + 1 + 1440
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--blocks", type=int, default=100_000, help="64 KiB blocks per GPU")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds):
+    """Oracle (C restatement, OpenMP over blocks) seal+open of a bounded sample."""
+    import numpy as np
+    from oracle import pyoracle as orc  # checker/baseline only
+    from rclone_amd.testdata import splitmix64_bytes
+
+    lib = orc.lib()
+    nb = 1024  # 64 MiB sample, repeated until `seconds` elapse
+    plain = np.frombuffer(splitmix64_bytes(0x5EED, nb * BLOCK_DATA), dtype=np.uint8).copy()
+    body = np.empty(nb * BLOCK_SIZE, dtype=np.uint8)
+    out = np.empty(nb * BLOCK_DATA, dtype=np.uint8)
+    ok = np.empty(nb, dtype=np.uint8)
+    key = splitmix64_bytes(1, 32)
+    n0 = splitmix64_bytes(2, 24)
+    vp = ctypes.c_void_p
+    threads = lib.orc_seal_blocks(vp(body.ctypes.data), vp(plain.ctypes.data), nb, n0, key)  # warm
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        threads = lib.orc_seal_blocks(vp(body.ctypes.data), vp(plain.ctypes.data), nb, n0, key)
+        lib.orc_open_blocks(vp(out.ctypes.data), vp(ok.ctypes.data), vp(body.ctypes.data), nb, n0, key)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    assert ok.all() and np.array_equal(out, plain)
+    gib = passes * 2 * nb * BLOCK_DATA / 2**30
+    return {"value": round(gib / el, 3), "unit": "GiB/s", "cores": int(threads), "kind": "port",
+            "sample": f"{passes} x (seal+open of {nb} x 64KiB blocks) = {gib:.1f} GiB in {el:.1f} s, "
+                      f"oracle/xsalsa_oracle.c OpenMP"}
+
+
+def load_traffic():
+    """HBM bytes per xs_crypt launch from the committed rocprofv3 PMC summary (or None)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("seal_bytes_per_launch"), d.get("open_bytes_per_launch"), d.get("source")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from rclone_amd import _lib, device
+    L = _lib.lib()
+    nb = args.blocks
+    plain_len = nb * BLOCK_DATA
+    body_len = nb * BLOCK_SIZE
+    key = bytes(range(32))
+    nonce0 = bytes([0x10 + rank]) + bytes(23)
+    plain = torch.empty(plain_len, dtype=torch.uint8, device=dev)
+    device.fill_random(plain, 0x5EED + rank)
+    body = torch.empty(body_len, dtype=torch.uint8, device=dev)
+    out = torch.empty(plain_len, dtype=torch.uint8, device=dev)
+    ok = torch.empty(nb, dtype=torch.uint8, device=dev)
+    ws_seal = device.workspace(nb, dev)
+    ws_open = device.workspace(nb, dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+
+    ev = []  # (seal?, start, end) around every xs_crypt launch
+
+    def step(record):
+        _lib.check(L.xs_keygen_object_dev(1, key, nonce0, 0, plain_len, ws_seal.data_ptr(), sp), "keygen")
+        if record:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+        _lib.check(L.xs_crypt_dev(1, ws_seal.data_ptr(), nb, plain.data_ptr(), body.data_ptr(), None, sp), "seal")
+        if record:
+            b.record(stream)
+            ev.append((True, a, b))
+        _lib.check(L.xs_keygen_object_dev(0, key, nonce0, 0, body_len, ws_open.data_ptr(), sp), "keygen")
+        if record:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+        _lib.check(L.xs_crypt_dev(0, ws_open.data_ptr(), nb, body.data_ptr(), out.data_ptr(), ok.data_ptr(), sp),
+                   "open")
+        if record:
+            b.record(stream)
+            ev.append((False, a, b))
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    # correctness gate before timing: round trip + every tag verified
+    if not (torch.equal(out, plain) and int(ok.sum()) == nb):
+        raise SystemExit("bench: round trip failed on rank %d" % rank)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    # counters and max time over ranks (RCCL, small tensors only)
+    counters = torch.tensor([args.steps * 2 * nb, args.steps * 2 * plain_len, int(nb - int(ok.sum()))],
+                            dtype=torch.int64, device=dev)
+    tmax = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    el = float(tmax.item())
+    seal_ms = [a.elapsed_time(b) for s, a, b in ev if s]
+    open_ms = [a.elapsed_time(b) for s, a, b in ev if not s]
+    seal_avg = sum(seal_ms) / len(seal_ms)
+    open_avg = sum(open_ms) / len(open_ms)
+    total_bytes = int(counters[1].item())
+    value = total_bytes / 2**30 / el
+    if rank == 0:
+        ach_seal = ALG_BYTES_SEAL * nb / (seal_avg * 1e-3) / 1e9
+        ach_open = ALG_BYTES_OPEN * nb / (open_avg * 1e-3) / 1e9
+        tr = load_traffic()
+        traffic = None
+        if tr and tr[0]:
+            traffic = {"seal": tr[0], "open": tr[1], "source": tr[2]}
+        res = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (SplitMix64 plaintext generated in HBM)",
+            "config": {"workload": f"{nb} x 64KiB device-resident blocks per GPU, seal then open+verify "
+                                   f"(BASELINE configs[1]+[2] shape)",
+                       "blocks_per_gpu": nb, "block_bytes": BLOCK_DATA,
+                       "parallelism": f"{world} rank(s), blocks sharded, no data-path collective"},
+            "seal_GiB_s": round(nb * BLOCK_DATA / 2**30 / (seal_avg * 1e-3), 3),
+            "open_GiB_s": round(nb * BLOCK_DATA / 2**30 / (open_avg * 1e-3), 3),
+            "roofline": {"bound": "hbm", "kernel": "xs_crypt<seal>",
+                         "achieved": round(ach_seal, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach_seal / HBM_PEAK_GBS, 4),
+                         "traffic": traffic["seal"] if traffic else None,
+                         "kernel_ms_avg": round(seal_avg, 4),
+                         "alg_bytes_per_launch": ALG_BYTES_SEAL * nb,
+                         "open": {"kernel": "xs_crypt<open>", "achieved": round(ach_open, 1),
+                                  "frac": round(ach_open / HBM_PEAK_GBS, 4), "kernel_ms_avg": round(open_avg, 4),
+                                  "traffic": traffic["open"] if traffic else None}},
+            "counters": {"blocks": int(counters[0].item()), "bytes": total_bytes,
+                         "tag_failures": int(counters[2].item())},
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu:
+            res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

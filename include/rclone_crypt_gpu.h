@@ -88,6 +88,15 @@ int xs_seal_batch_dev(const uint8_t key[32], const xs_block_desc *d_desc, uint64
 int xs_open_batch_dev(const uint8_t key[32], const xs_block_desc *d_desc, uint64_t nblocks,
                       const void *d_src, uint64_t src_len, void *d_dst, uint64_t dst_len, uint8_t *d_ok,
                       void *d_workspace, void *stream);
+/* The two halves of xs_seal_object_dev / xs_open_object_dev, for callers that pipeline or
+ * time the kernels separately: xs_keygen_object_dev writes the per-block key schedule
+ * (nonce, HSalsa20 subkey, Poly1305 key and power tables) into d_workspace for the object
+ * range (len = plaintext bytes when seal != 0, wire-body bytes otherwise); xs_crypt_dev then
+ * runs the block kernel over nblocks blocks of that schedule. */
+int xs_keygen_object_dev(int seal, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                         uint64_t len, void *d_workspace, void *stream);
+int xs_crypt_dev(int seal, const void *d_workspace, uint64_t nblocks, const void *d_src, void *d_dst,
+                 uint8_t *d_ok, void *stream);
 /* Fill d with the SplitMix64 stream (word k = mix(seed + (k+1)*0x9E3779B97F4A7C15)). */
 int xs_fill_random_dev(void *d, uint64_t nbytes, uint64_t seed, void *stream);
 

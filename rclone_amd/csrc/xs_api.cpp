@@ -158,6 +158,37 @@ int xs_open_batch_dev(const uint8_t key[32], const xs_block_desc* d_desc, uint64
   return XS_OK;
 }
 
+int xs_keygen_object_dev(int seal, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                         uint64_t len, void* d_workspace, void* stream) {
+  if (!key || !nonce0 || !d_workspace || !aligned16(d_workspace)) {
+    set_error("xs_keygen_object_dev: bad argument");
+    return XS_ERR_INVALID;
+  }
+  if (len == 0) return XS_OK;
+  const uint64_t unit = seal ? XS_BLOCK_DATA : XS_BLOCK_SIZE;
+  const uint64_t nblocks = (len + unit - 1) / unit;
+  if (!seal && len - (nblocks - 1) * XS_BLOCK_SIZE <= XS_BLOCK_HDR) {
+    set_error("xs_keygen_object_dev: truncated block header");
+    return XS_ERR_INVALID;
+  }
+  hipError_t e = launch_keygen(seal ? 0 : 1, key_arg(key), nonce_arg(nonce0), first_block, len, nblocks, nullptr,
+                               (BlockKey*)d_workspace, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "keygen launch");
+  return XS_OK;
+}
+
+int xs_crypt_dev(int seal, const void* d_workspace, uint64_t nblocks, const void* d_src, void* d_dst, uint8_t* d_ok,
+                 void* stream) {
+  if (!d_workspace || !d_src || !d_dst || (!seal && !d_ok)) {
+    set_error("xs_crypt_dev: null argument");
+    return XS_ERR_INVALID;
+  }
+  hipError_t e = launch_crypt(seal != 0, (const BlockKey*)d_workspace, nblocks, (const uint8_t*)d_src,
+                              (uint8_t*)d_dst, d_ok, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "crypt launch");
+  return XS_OK;
+}
+
 int xs_fill_random_dev(void* d, uint64_t nbytes, uint64_t seed, void* stream) {
   if (!d || (nbytes & 7u) || !aligned16(d)) {
     set_error("xs_fill_random_dev: need a 16-byte aligned buffer and a multiple of 8 bytes");

@@ -29,9 +29,16 @@
 
 #include "xs_internal.h"
 
+// XS_WAVES_PER_EU: occupancy hint for diagnostic builds (tools/ablate.cpp); product = 1.
+#ifndef XS_WAVES_PER_EU
+#define XS_WAVES_PER_EU 1
+#endif
+
+
 namespace xs {
 
 constexpr uint32_t M26 = 0x3ffffffu;
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 struct P5 {
   uint32_t v[5];
@@ -51,8 +58,10 @@ __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, int s) {
   d ^= rotl(c + b, 13);          \
   a ^= rotl(d + c, 18);
 
+// The double-round loop is deliberately not unrolled: fully unrolled, the scheduler hoists
+// across rounds and the kernel needs ~90 VGPRs; rolled it needs ~20 and measured faster.
 __device__ __forceinline__ void salsa_rounds(uint32_t (&x)[16]) {
-#pragma unroll
+#pragma unroll 1
   for (int i = 0; i < 10; i++) {
     XS_QR(x[0], x[4], x[8], x[12]);
     XS_QR(x[5], x[9], x[13], x[1]);
@@ -355,24 +364,28 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
 // SEAL: in = plaintext block, out = tag(16) || ct.   OPEN: in = tag || ct, out = plaintext,
 // ok[blk] = 1 if the tag verified (else the plaintext is zero-filled, the
 // pass_bad_blocks contract of cipher.go:885-893).
-template <bool SEAL>
-__global__ void __launch_bounds__(256) xs_crypt(const BlockKey* __restrict__ keys, const uint8_t* __restrict__ src,
-                                                uint8_t* __restrict__ dst, uint8_t* __restrict__ ok) {
-  __shared__ uint32_t red[4][5];
-  __shared__ uint32_t verdict;
-  const BlockKey* bk = keys + blockIdx.x;
-  if (bk->flags) {  // rejected descriptor: write nothing
-    if (!SEAL && threadIdx.x == 0) ok[blockIdx.x] = 0;
-    return;
-  }
-  const uint32_t n = bk->len;
-  const uint8_t* in = src + bk->src;
-  uint8_t* out = dst + bk->dst;
-  const uint8_t* pin = SEAL ? in : in + XS_BLOCK_HDR;
-  uint8_t* pout = SEAL ? out + XS_BLOCK_HDR : out;
-  const uint32_t t = threadIdx.x;
-  const int nc = (int)((n + 15u) >> 4);
+//
+// Per group s (s = 0..3) lane t owns keystream block K = t + 256 s and message chunks
+// 4K-2 .. 4K+1.  The wave's 4 KiB of input for the group is staged into its own LDS slot by
+// global_load_lds_dwordx4 (no VGPRs held across the 20 Salsa20 rounds), read back after the
+// keystream is ready, XORed and stored.  Lane 255 also owns chunks 4094, 4095 (keystream
+// block 1024, precomputed by keygen), so every lane's Horner multipliers are uniform:
+// r inside a group, r^1021 between groups.
+constexpr int LDS_WORDS = 4 * 1024 + 32;
+typedef __attribute__((address_space(3))) void lds_void;
 
+__device__ __forceinline__ uint32_t keep_mask(uint32_t L, uint32_t i) {
+  // mask of the bytes of word i (bytes 4i..4i+3) that lie below L
+  return (L >= 4u * i + 4u) ? 0xffffffffu : (L <= 4u * i ? 0u : ((1u << (8u * (L - 4u * i))) - 1u));
+}
+
+template <bool SEAL, bool FULL>
+__device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, const uint8_t* __restrict__ pin,
+                                            uint8_t* __restrict__ pout, uint32_t n, uint32_t* lds, P5& h) {
+  const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+  uint32_t* wb = lds + wave * 1024u;  // this wave's 4 KiB staging slot
+  const int nc = FULL ? 4096 : (int)((n + 15u) >> 4);
+  const int nfull = FULL ? 4096 : (int)(n >> 4);  // chunks that are whole 16-byte chunks
   uint32_t k[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) k[i] = bk->subkey[i];
@@ -384,130 +397,161 @@ __global__ void __launch_bounds__(256) xs_crypt(const BlockKey* __restrict__ key
     RR.v[i] = bk->R[i];
   }
   const PMul Mr = pmul_prep(rr), MR = pmul_prep(RR);
-
-  P5 h;
-  h.v[0] = h.v[1] = h.v[2] = h.v[3] = h.v[4] = 0;
   int c_last = -1;
+  P5 t1, t2;
 
 #pragma unroll 1
   for (int s = 0; s < 4; s++) {
     const uint32_t K = t + 256u * (uint32_t)s;
     const int cfirst = 4 * (int)K - 2;
-    if (cfirst >= nc) break;
-    const bool has_next = (cfirst + 1024) < nc;
-    const bool fast = (K > 0) && (64u * K + 32u <= n);
-    uint32_t d[16];
-    if (fast) {
-      const uint4* p = reinterpret_cast<const uint4*>(pin + 64u * K - 32u);
+    if (!FULL && cfirst >= nc) break;
+    // stage this group's input (whole chunks only) into the wave's LDS slot
+    const uint8_t* src = pin + 64u * K - 32u;
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        uint4 v = p[j];
-        d[4 * j] = v.x; d[4 * j + 1] = v.y; d[4 * j + 2] = v.z; d[4 * j + 3] = v.w;
+    for (int j = 0; j < 4; j++) {
+      const int c = cfirst + j;
+      const bool whole = FULL ? (c >= 0) : (c >= 0 && c < nfull);
+      if (whole) __builtin_amdgcn_global_load_lds(src + 16 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
+    }
+    if (s == 3) {  // final-exponent tables, needed after the loop
+      const uint32_t e = FULL ? ((t == 255u) ? 0u : 1022u - 4u * t) : 0u;
+      if (FULL) {
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          t1.v[i] = bk->T1[e & 31u][i];
+          t2.v[i] = bk->T2[e >> 5][i];
+        }
       }
     }
     uint32_t ks[16];
     salsa20_block(k, n0, n1, K, ks);
-    if (fast) {
-      uint32_t o[16];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t d[16];
 #pragma unroll
-      for (int i = 0; i < 16; i++) o[i] = d[i] ^ ks[i];
-      uint4* q = reinterpret_cast<uint4*>(pout + 64u * K - 32u);
+    for (int j = 0; j < 4; j++) {
+      uint4 v = *reinterpret_cast<const uint4*>(wb + 256 * j + 4 * lane);
+      d[4 * j] = v.x; d[4 * j + 1] = v.y; d[4 * j + 2] = v.z; d[4 * j + 3] = v.w;
+    }
+    uint32_t plen[4];  // bytes of each chunk (16 whole, 0 absent, else partial)
 #pragma unroll
-      for (int j = 0; j < 4; j++) q[j] = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
-      const uint32_t* c = SEAL ? o : d;  // Poly1305 runs over the ciphertext
-#pragma unroll
-      for (int j = 0; j < 3; j++) {
-        padd_full(h, c[4 * j], c[4 * j + 1], c[4 * j + 2], c[4 * j + 3]);
-        h = pmul_u(h, Mr);
-      }
-      padd_full(h, c[12], c[13], c[14], c[15]);
-      {
-        PMul M3;
-#pragma unroll
-        for (int i = 0; i < 5; i++) {
-          M3.m[i] = has_next ? MR.m[i] : Mr.m[i];
-          M3.s[i] = has_next ? MR.s[i] : Mr.s[i];
-        }
-        h = pmul_u(h, M3);
-      }
-      c_last = cfirst + 3;
-    } else {
-      // boundary group: K == 0 (first two chunks are the Poly1305 key) or the block tail
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int c = cfirst + j;
-        if (c < 0 || c >= nc) continue;
-        const uint32_t off = 16u * (uint32_t)c;
-        const uint32_t L = (n - off) < 16u ? (n - off) : 16u;
-        uint32_t w[4];
-        if (L == 16u) {
-          uint4 v = *reinterpret_cast<const uint4*>(pin + off);
-          w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-        } else {
-          uint8_t bb[16];
-#pragma unroll
-          for (int i = 0; i < 16; i++) bb[i] = (uint32_t)i < L ? pin[off + i] : 0;
-#pragma unroll
-          for (int i = 0; i < 4; i++)
-            w[i] = (uint32_t)bb[4 * i] | ((uint32_t)bb[4 * i + 1] << 8) | ((uint32_t)bb[4 * i + 2] << 16) |
-                   ((uint32_t)bb[4 * i + 3] << 24);
-        }
-        uint32_t o4[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) o4[i] = w[i] ^ ks[4 * j + i];
-        if (L < 16u) {
-          // keep only the first L bytes of the output chunk
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const int lo = 4 * i;
-            uint32_t keep = (L >= (uint32_t)lo + 4u) ? 0xffffffffu
-                            : (L <= (uint32_t)lo ? 0u : ((1u << (8u * (L - (uint32_t)lo))) - 1u));
-            o4[i] &= keep;
-            w[i] &= keep;
-          }
-        }
-        if (L == 16u) {
-          *reinterpret_cast<uint4*>(pout + off) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
-        } else {
-          for (uint32_t i = 0; i < L; i++) pout[off + i] = (uint8_t)(o4[i >> 2] >> (8u * (i & 3u)));
-        }
-        uint32_t cw[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) cw[i] = SEAL ? o4[i] : w[i];
-        if (L == 16u) {
-          padd_full(h, cw[0], cw[1], cw[2], cw[3]);
-        } else {
-          // pad byte 0x01 at position L
-          cw[L >> 2] |= 1u << (8u * (L & 3u));
-          padd_part(h, cw[0], cw[1], cw[2], cw[3]);
-        }
-        if (j == 3 && has_next) h = pmul_u(h, MR);
-        else h = pmul_u(h, Mr);
-        c_last = c;
+    for (int j = 0; j < 4; j++) {
+      const int c = cfirst + j;
+      if (FULL) {
+        plen[j] = (c >= 0) ? 16u : 0u;
+      } else {
+        plen[j] = (c < 0 || c >= nc) ? 0u : ((c < nfull) ? 16u : (n & 15u));
       }
     }
+    if (!FULL) {
+      // the block's last chunk may be partial: byte loads by its owner
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (plen[j] != 0u && plen[j] != 16u) {
+          const uint32_t off = 16u * (uint32_t)(cfirst + j);
+          uint32_t w[4] = {0, 0, 0, 0};
+          for (uint32_t i = 0; i < plen[j]; i++) w[i >> 2] |= (uint32_t)pin[off + i] << (8u * (i & 3u));
+          d[4 * j] = w[0]; d[4 * j + 1] = w[1]; d[4 * j + 2] = w[2]; d[4 * j + 3] = w[3];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (plen[j] == 0u) { d[4 * j] = 0; d[4 * j + 1] = 0; d[4 * j + 2] = 0; d[4 * j + 3] = 0; }
+    }
+    uint32_t o[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) o[i] = d[i] ^ ks[i];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {  // absent chunks (the Poly1305 key slots of K = 0) hash as zero
+      if (plen[j] == 0u) { o[4 * j] = 0; o[4 * j + 1] = 0; o[4 * j + 2] = 0; o[4 * j + 3] = 0; }
+    }
+    if (!FULL) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (plen[j] != 16u) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) o[4 * j + i] &= keep_mask(plen[j], (uint32_t)i);
+        }
+      }
+    }
+    uint8_t* dst = pout + 64u * K - 32u;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (plen[j] == 16u) {
+        *reinterpret_cast<uint4*>(dst + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
+      } else if (!FULL && plen[j] != 0u) {
+        for (uint32_t i = 0; i < plen[j]; i++) dst[16 * j + i] = (uint8_t)(o[4 * j + (i >> 2)] >> (8u * (i & 3u)));
+      }
+    }
+    // Poly1305 over the ciphertext: (h + c) * r within the group, * r^1021 (or r) at its end
+    const uint32_t* cw = SEAL ? o : d;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (FULL) {
+        const uint32_t pad = (s == 0 && j < 2) ? ((t == 0u) ? 0u : (1u << 24)) : (1u << 24);
+        h.v[0] += cw[4 * j] & M26;
+        h.v[1] += alignbit(cw[4 * j + 1], cw[4 * j], 26) & M26;
+        h.v[2] += alignbit(cw[4 * j + 2], cw[4 * j + 1], 20) & M26;
+        h.v[3] += alignbit(cw[4 * j + 3], cw[4 * j + 2], 14) & M26;
+        h.v[4] += (cw[4 * j + 3] >> 8) | pad;
+        h = pmul_u(h, (j == 3 && s < 3) ? MR : Mr);
+      } else {
+        if (plen[j] != 0u) {
+          uint32_t w0 = cw[4 * j], w1 = cw[4 * j + 1], w2 = cw[4 * j + 2], w3 = cw[4 * j + 3];
+          uint32_t pad = 1u << 24;
+          if (plen[j] != 16u) {  // 0x01 after the last byte, no 2^128 bit
+            const uint32_t L = plen[j];
+            const uint32_t bit = 1u << (8u * (L & 3u));
+            w0 |= (L >> 2) == 0u ? bit : 0u;
+            w1 |= (L >> 2) == 1u ? bit : 0u;
+            w2 |= (L >> 2) == 2u ? bit : 0u;
+            w3 |= (L >> 2) == 3u ? bit : 0u;
+            pad = 0u;
+          }
+          h.v[0] += w0 & M26;
+          h.v[1] += alignbit(w1, w0, 26) & M26;
+          h.v[2] += alignbit(w2, w1, 20) & M26;
+          h.v[3] += alignbit(w3, w2, 14) & M26;
+          h.v[4] += (w3 >> 8) | pad;
+          const bool use_R = (j == 3) && (s < 3) && (cfirst + 1024 < nc);
+          PMul M;
+#pragma unroll
+          for (int i = 0; i < 5; i++) {
+            M.m[i] = use_R ? MR.m[i] : Mr.m[i];
+            M.s[i] = use_R ? MR.s[i] : Mr.s[i];
+          }
+          h = pmul_u(h, M);
+          c_last = cfirst + j;
+        }
+      }
+    }
+    if (FULL) c_last = cfirst + 3;
   }
-  // lane 0 also owns chunks 4094, 4095 (keystream block 1024, precomputed by keygen)
-  if (t == 0 && nc > 4094) {
+  // lane 255 owns chunks 4094, 4095 (keystream block 1024 words 0..7)
+  if (t == 255u && nc > 4094) {
 #pragma unroll 1
     for (int j = 0; j < 2; j++) {
       const int c = 4094 + j;
       if (c >= nc) break;
       const uint32_t off = 16u * (uint32_t)c;
-      const uint32_t L = (n - off) < 16u ? (n - off) : 16u;
+      const uint32_t L = FULL ? 16u : ((n - off) < 16u ? (n - off) : 16u);
       uint32_t w[4], o4[4];
-      for (int i = 0; i < 4; i++) {
-        uint32_t v = 0;
-        for (int bI = 0; bI < 4; bI++) {
-          uint32_t pos = 4u * i + bI;
-          if (pos < L) v |= (uint32_t)pin[off + pos] << (8 * bI);
-        }
-        w[i] = v;
-        uint32_t keep = (L >= 4u * i + 4u) ? 0xffffffffu : (L <= 4u * i ? 0u : ((1u << (8u * (L - 4u * i))) - 1u));
-        o4[i] = (v ^ bk->ks1024[4 * j + i]) & keep;
+      if (L == 16u) {
+        const uint4 v = *reinterpret_cast<const uint4*>(pin + off);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+      } else {
+        w[0] = w[1] = w[2] = w[3] = 0;
+        for (uint32_t i = 0; i < L; i++) w[i >> 2] |= (uint32_t)pin[off + i] << (8u * (i & 3u));
       }
-      for (uint32_t i = 0; i < L; i++) pout[off + i] = (uint8_t)(o4[i >> 2] >> (8u * (i & 3u)));
+#pragma unroll
+      for (int i = 0; i < 4; i++) o4[i] = (w[i] ^ bk->ks1024[4 * j + i]) & keep_mask(L, (uint32_t)i);
+      if (L == 16u) {
+        *reinterpret_cast<uint4*>(pout + off) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+      } else {
+        for (uint32_t i = 0; i < L; i++) pout[off + i] = (uint8_t)(o4[i >> 2] >> (8u * (i & 3u)));
+      }
       uint32_t cw[4];
+#pragma unroll
       for (int i = 0; i < 4; i++) cw[i] = SEAL ? o4[i] : w[i];
       if (L == 16u) {
         padd_full(h, cw[0], cw[1], cw[2], cw[3]);
@@ -519,17 +563,47 @@ __global__ void __launch_bounds__(256) xs_crypt(const BlockKey* __restrict__ key
       c_last = c;
     }
   }
-  // bring every lane's partial to exponent 0: multiply by r^(nc-1-c_last)
-  if (c_last >= 0) {
-    const uint32_t e = (uint32_t)(nc - 1 - c_last);
-    P5 t1, t2;
+  // bring the lane's partial sum to exponent 0: * r^(nc-1-c_last)
+  if (!FULL) {
+    if (c_last >= 0) {
+      const uint32_t e = (uint32_t)(nc - 1 - c_last);
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
-      t1.v[i] = bk->T1[e & 31u][i];
-      t2.v[i] = bk->T2[e >> 5][i];
+      for (int i = 0; i < 5; i++) {
+        t1.v[i] = bk->T1[e & 31u][i];
+        t2.v[i] = bk->T2[e >> 5][i];
+      }
+      h = pmul(h, pmul(t1, t2));
     }
+  } else {
     h = pmul(h, pmul(t1, t2));
   }
+}
+
+template <bool SEAL>
+__global__ void __launch_bounds__(256, XS_WAVES_PER_EU) xs_crypt(const BlockKey* __restrict__ keys,
+                                                                 const uint8_t* __restrict__ src,
+                                                                 uint8_t* __restrict__ dst,
+                                                                 uint8_t* __restrict__ ok) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
+  const BlockKey* bk = keys + blockIdx.x;
+  if (bk->flags) {  // rejected descriptor: write nothing
+    if (!SEAL && threadIdx.x == 0) ok[blockIdx.x] = 0;
+    return;
+  }
+  const uint32_t n = bk->len;
+  const uint8_t* in = src + bk->src;
+  uint8_t* out = dst + bk->dst;
+  const uint8_t* pin = SEAL ? in : in + XS_BLOCK_HDR;
+  uint8_t* pout = SEAL ? out + XS_BLOCK_HDR : out;
+  const uint32_t t = threadIdx.x;
+
+  P5 h;
+  h.v[0] = h.v[1] = h.v[2] = h.v[3] = h.v[4] = 0;
+  if (n == XS_BLOCK_DATA) crypt_block<SEAL, true>(bk, pin, pout, n, lds, h);
+#ifndef XS_ONLY_FULL
+  else crypt_block<SEAL, false>(bk, pin, pout, n, lds, h);
+#endif
+
   // sum the 256 partials: wave shuffles, then LDS across the 4 waves
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
@@ -537,17 +611,18 @@ __global__ void __launch_bounds__(256) xs_crypt(const BlockKey* __restrict__ key
     for (int i = 0; i < 5; i++) h.v[i] += (uint32_t)__shfl_xor((int)h.v[i], off, 64);
     if (off == 2) pnorm(h);
   }
+  uint32_t* red = lds + 4 * 1024;
   const uint32_t wave = t >> 6, lane = t & 63u;
   if (!SEAL) __builtin_amdgcn_s_waitcnt(0);  // our plaintext stores complete before a possible zero-fill
   if (lane == 0) {
 #pragma unroll
-    for (int i = 0; i < 5; i++) red[wave][i] = h.v[i];
+    for (int i = 0; i < 5; i++) red[wave * 5 + i] = h.v[i];
   }
   __syncthreads();
   if (t == 0) {
     P5 acc;
 #pragma unroll
-    for (int i = 0; i < 5; i++) acc.v[i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    for (int i = 0; i < 5; i++) acc.v[i] = red[i] + red[5 + i] + red[10 + i] + red[15 + i];
     P5 hc = pcanon(acc);
     uint32_t s4[4] = {bk->s[0], bk->s[1], bk->s[2], bk->s[3]};
     uint32_t tag[4];
@@ -557,13 +632,13 @@ __global__ void __launch_bounds__(256) xs_crypt(const BlockKey* __restrict__ key
     } else {
       uint4 want = *reinterpret_cast<const uint4*>(in);
       uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) | (want.z ^ tag[2]) | (want.w ^ tag[3]);
-      verdict = diff == 0 ? 1u : 0u;
+      red[20] = diff == 0 ? 1u : 0u;
       ok[blockIdx.x] = diff == 0 ? 1 : 0;
     }
   }
   if (!SEAL) {
     __syncthreads();
-    if (verdict == 0) {
+    if (red[20] == 0) {
       // authentication failed: zero the block's plaintext (ordered after the stores above)
       for (uint32_t off = 16u * t; off < n; off += 16u * 256u) {
         const uint32_t L = (n - off) < 16u ? (n - off) : 16u;

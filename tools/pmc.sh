@@ -1,0 +1,19 @@
+#!/bin/bash
+# PMC passes for the crypt kernels (run on the GPU box via gpurun).  Each counter group is
+# its own rocprofv3 run (no tracing domains combined with --pmc).
+# usage: tools/pmc.sh <outdir-under-gpurun_out> [bench args...]
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$1; shift
+ARGS="$@"
+export TMPDIR=/tmp
+cd /tmp
+i=0
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY" \
+           "FETCH_SIZE" "WRITE_SIZE" \
+           "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 GRBM_GUI_ACTIVE SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_ACTIVE_INST_ANY" \
+           "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_WRREQ TCC_EA0_WRREQ_64B"; do
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -- python3 $R/bench.py $ARGS > $OUT.p$i.log 2>&1
+  i=$((i+1))
+done
+echo pmc_done
