@@ -60,9 +60,9 @@ __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, int s) {
 
 // The double-round loop is deliberately not unrolled: fully unrolled, the scheduler hoists
 // across rounds and the kernel needs ~90 VGPRs; rolled it needs ~20 and measured faster.
-__device__ __forceinline__ void salsa_rounds(uint32_t (&x)[16]) {
+__device__ __forceinline__ void salsa_rounds_n(uint32_t (&x)[16], int nd) {
 #pragma unroll 1
-  for (int i = 0; i < 10; i++) {
+  for (int i = 0; i < nd; i++) {
     XS_QR(x[0], x[4], x[8], x[12]);
     XS_QR(x[5], x[9], x[13], x[1]);
     XS_QR(x[10], x[14], x[2], x[6]);
@@ -74,8 +74,12 @@ __device__ __forceinline__ void salsa_rounds(uint32_t (&x)[16]) {
   }
 }
 
+__device__ __forceinline__ void salsa_rounds(uint32_t (&x)[16]) { salsa_rounds_n(x, 10); }
+__device__ __forceinline__ void salsa_rounds9(uint32_t (&x)[16]) { salsa_rounds_n(x, 9); }
+
 constexpr uint32_t SIG0 = 0x61707865u, SIG1 = 0x3320646eu, SIG2 = 0x79622d32u, SIG3 = 0x6b206574u;
 
+// Salsa20/20 keystream block `ctr` for a 32-byte key (k[8]) and 8-byte nonce (n0, n1).
 // Salsa20/20 keystream block `ctr` for a 32-byte key (k[8]) and 8-byte nonce (n0, n1).
 __device__ __forceinline__ void salsa20_block(const uint32_t (&k)[8], uint32_t n0, uint32_t n1,
                                               uint32_t ctr, uint32_t (&out)[16]) {
@@ -97,6 +101,88 @@ __device__ __forceinline__ void salsa20_block(const uint32_t (&k)[8], uint32_t n
   out[12] = x[12] + k[5];
   out[13] = x[13] + k[6];
   out[14] = x[14] + k[7];
+  out[15] = x[15] + SIG3;
+}
+
+// First double round, partially evaluated.  With key and nonce wave-uniform only the block
+// counter (word 8) differs between lanes; 60 of the round's 96 add/rotate/xor steps do not
+// depend on it and are computed once per workgroup (SalsaPre), the other 36 per block.
+struct SalsaPre {
+  uint32_t k[8], n0, n1;
+  uint32_t x4, u9;                 // column QR(0,4,8,12): x4 final, rotl(x4 + x0, 9)
+  uint32_t x1, x2, x3;             // column-round outputs feeding row QR(0,1,2,3)
+  uint32_t x4r, x5r, x6r, x7r;     // row QR(5,6,7,4): fully uniform
+  uint32_t x9, x10, x11r, v9;      // row QR(10,11,8,9): first step uniform; v9 = rotl(x11r + x10, 9)
+  uint32_t x13, x14, x15, w7;      // row QR(15,12,13,14): w7 = rotl(x15 + x14, 7)
+};
+
+__device__ __forceinline__ uint32_t rotl_u(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+__device__ __forceinline__ SalsaPre salsa_pre(const uint32_t (&k)[8], uint32_t n0, uint32_t n1) {
+  SalsaPre p;
+#pragma unroll
+  for (int i = 0; i < 8; i++) p.k[i] = k[i];
+  p.n0 = n0;
+  p.n1 = n1;
+  // column round
+  uint32_t x0 = SIG0, x4 = k[3], x12 = k[5];
+  x4 ^= rotl_u(x0 + x12, 7);
+  p.x4 = x4;
+  p.u9 = rotl_u(x4 + x0, 9);
+  uint32_t x5 = SIG1, x9 = 0, x13 = k[6], x1 = k[0];
+  x9 ^= rotl_u(x5 + x1, 7); x13 ^= rotl_u(x9 + x5, 9); x1 ^= rotl_u(x13 + x9, 13); x5 ^= rotl_u(x1 + x13, 18);
+  uint32_t x10 = SIG2, x14 = k[7], x2 = k[1], x6 = n0;
+  x14 ^= rotl_u(x10 + x6, 7); x2 ^= rotl_u(x14 + x10, 9); x6 ^= rotl_u(x2 + x14, 13); x10 ^= rotl_u(x6 + x2, 18);
+  uint32_t x15 = SIG3, x3 = k[2], x7 = n1, x11 = k[4];
+  x3 ^= rotl_u(x15 + x11, 7); x7 ^= rotl_u(x3 + x15, 9); x11 ^= rotl_u(x7 + x3, 13); x15 ^= rotl_u(x11 + x7, 18);
+  p.x1 = x1; p.x2 = x2; p.x3 = x3;
+  // row round, uniform parts
+  x6 ^= rotl_u(x5 + x4, 7); x7 ^= rotl_u(x6 + x5, 9); x4 ^= rotl_u(x7 + x6, 13); x5 ^= rotl_u(x4 + x7, 18);
+  p.x4r = x4; p.x5r = x5; p.x6r = x6; p.x7r = x7;
+  x11 ^= rotl_u(x10 + x9, 7);
+  p.x9 = x9; p.x10 = x10; p.x11r = x11; p.v9 = rotl_u(x11 + x10, 9);
+  p.x13 = x13; p.x14 = x14; p.x15 = x15; p.w7 = rotl_u(x15 + x14, 7);
+  return p;
+}
+
+// Keystream block `ctr` from the precomputed first-round values (bit-identical to
+// salsa20_block).
+__device__ __forceinline__ void salsa20_block_pre(const SalsaPre& p, uint32_t ctr, uint32_t (&out)[16]) {
+  uint32_t x[16];
+  // column QR(0,4,8,12) lane part
+  x[8] = ctr ^ p.u9;
+  x[12] = p.k[5] ^ rotl(x[8] + p.x4, 13);
+  x[0] = SIG0 ^ rotl(x[12] + x[8], 18);
+  // row QR(0,1,2,3)
+  x[1] = p.x1; x[2] = p.x2; x[3] = p.x3;
+  XS_QR(x[0], x[1], x[2], x[3]);
+  x[4] = p.x4r; x[5] = p.x5r; x[6] = p.x6r; x[7] = p.x7r;
+  // row QR(10,11,8,9)
+  x[11] = p.x11r;
+  x[8] ^= p.v9;
+  x[9] = p.x9 ^ rotl(x[8] + x[11], 13);
+  x[10] = p.x10 ^ rotl(x[9] + x[8], 18);
+  // row QR(15,12,13,14)
+  x[12] ^= p.w7;
+  x[13] = p.x13 ^ rotl(x[12] + p.x15, 9);
+  x[14] = p.x14 ^ rotl(x[13] + x[12], 13);
+  x[15] = p.x15 ^ rotl(x[14] + x[13], 18);
+  salsa_rounds9(x);
+  out[0] = x[0] + SIG0;
+  out[1] = x[1] + p.k[0];
+  out[2] = x[2] + p.k[1];
+  out[3] = x[3] + p.k[2];
+  out[4] = x[4] + p.k[3];
+  out[5] = x[5] + SIG1;
+  out[6] = x[6] + p.n0;
+  out[7] = x[7] + p.n1;
+  out[8] = x[8] + ctr;
+  out[9] = x[9];
+  out[10] = x[10] + SIG2;
+  out[11] = x[11] + p.k[4];
+  out[12] = x[12] + p.k[5];
+  out[13] = x[13] + p.k[6];
+  out[14] = x[14] + p.k[7];
   out[15] = x[15] + SIG3;
 }
 
@@ -389,7 +475,7 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
   uint32_t k[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) k[i] = bk->subkey[i];
-  const uint32_t n0 = bk->n2[0], n1 = bk->n2[1];
+  const SalsaPre pre = salsa_pre(k, bk->n2[0], bk->n2[1]);
   P5 rr, RR;
 #pragma unroll
   for (int i = 0; i < 5; i++) {
@@ -424,7 +510,7 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
       }
     }
     uint32_t ks[16];
-    salsa20_block(k, n0, n1, K, ks);
+    salsa20_block_pre(pre, K, ks);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t d[16];
 #pragma unroll
@@ -437,7 +523,8 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
     for (int j = 0; j < 4; j++) {
       const int c = cfirst + j;
       if (FULL) {
-        plen[j] = (c >= 0) ? 16u : 0u;
+        plen[j] = 16u;
+        (void)c;
       } else {
         plen[j] = (c < 0 || c >= nc) ? 0u : ((c < nfull) ? 16u : (n & 15u));
       }
@@ -454,16 +541,20 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
         }
       }
     }
+    if (!FULL) {
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      if (plen[j] == 0u) { d[4 * j] = 0; d[4 * j + 1] = 0; d[4 * j + 2] = 0; d[4 * j + 3] = 0; }
+      for (int j = 0; j < 4; j++) {
+        if (plen[j] == 0u) { d[4 * j] = 0; d[4 * j + 1] = 0; d[4 * j + 2] = 0; d[4 * j + 3] = 0; }
+      }
     }
     uint32_t o[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) o[i] = d[i] ^ ks[i];
+    if (!FULL) {
 #pragma unroll
-    for (int j = 0; j < 4; j++) {  // absent chunks (the Poly1305 key slots of K = 0) hash as zero
-      if (plen[j] == 0u) { o[4 * j] = 0; o[4 * j + 1] = 0; o[4 * j + 2] = 0; o[4 * j + 3] = 0; }
+      for (int j = 0; j < 4; j++) {  // absent chunks hash as zero
+        if (plen[j] == 0u) { o[4 * j] = 0; o[4 * j + 1] = 0; o[4 * j + 2] = 0; o[4 * j + 3] = 0; }
+      }
     }
     if (!FULL) {
 #pragma unroll
@@ -475,9 +566,13 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
       }
     }
     uint8_t* dst = pout + 64u * K - 32u;
+    const bool key_slots = FULL && s == 0 && t == 0u;  // chunks -2, -1 of K = 0: the Poly1305 key
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      if (plen[j] == 16u) {
+      if (FULL) {
+        if (j >= 2 || !key_slots)
+          *reinterpret_cast<uint4*>(dst + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
+      } else if (plen[j] == 16u) {
         *reinterpret_cast<uint4*>(dst + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
       } else if (!FULL && plen[j] != 0u) {
         for (uint32_t i = 0; i < plen[j]; i++) dst[16 * j + i] = (uint8_t)(o[4 * j + (i >> 2)] >> (8u * (i & 3u)));
@@ -488,13 +583,11 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       if (FULL) {
-        const uint32_t pad = (s == 0 && j < 2) ? ((t == 0u) ? 0u : (1u << 24)) : (1u << 24);
-        h.v[0] += cw[4 * j] & M26;
-        h.v[1] += alignbit(cw[4 * j + 1], cw[4 * j], 26) & M26;
-        h.v[2] += alignbit(cw[4 * j + 2], cw[4 * j + 1], 20) & M26;
-        h.v[3] += alignbit(cw[4 * j + 3], cw[4 * j + 2], 14) & M26;
-        h.v[4] += (cw[4 * j + 3] >> 8) | pad;
+        padd_full(h, cw[4 * j], cw[4 * j + 1], cw[4 * j + 2], cw[4 * j + 3]);
         h = pmul_u(h, (j == 3 && s < 3) ? MR : Mr);
+        if (j == 1 && key_slots) {  // discard what lane 0 hashed for the key slots
+          h.v[0] = h.v[1] = h.v[2] = h.v[3] = h.v[4] = 0;
+        }
       } else {
         if (plen[j] != 0u) {
           uint32_t w0 = cw[4 * j], w1 = cw[4 * j + 1], w2 = cw[4 * j + 2], w3 = cw[4 * j + 3];
