@@ -1,0 +1,685 @@
+// cipher.cpp -- host mirror of the data half of rclone's backend/crypt/cipher.go (v1.76.0)
+// behind the rc_* C ABI (include/rclone_crypt_gpu.h).
+//
+// Same names, argument meaning, error values and error precedence as the reference:
+//   Cipher/newCipher/Key          cipher.go:172-252   (rc_cipher_new, rc_cipher_key)
+//   nonce carry/increment/add     cipher.go:621-678   (rc_nonce_*)
+//   encrypter / newEncrypter / Read / finish / EncryptData   cipher.go:681-774
+//   decrypter / newDecrypter / newDecrypterSeek / fillBuffer / Read / RangeSeek / Seek /
+//   finish / unFinish / Close / finishAndClose / DecryptData / DecryptDataSeek
+//                                 cipher.go:776-1118
+//   calculateUnderlying           cipher.go:935-965
+//   EncryptedSize / DecryptedSize cipher.go:1121-1146
+//
+// What differs is only *when* blocks are sealed/opened: instead of one secretbox call per
+// 64 KiB block (cipher.go:737, :880) a handle ReadFills up to batch_blocks blocks from the
+// underlying reader in the reference's exact call sequence (a short or failed ReadFill ends
+// the batch, so the reader sees the same Read calls, just earlier) and seals/opens them in
+// one GPU submission through the xs_engine.  Bytes returned, errors returned, the position
+// at which each error surfaces and the nonce after EOF are those of the reference.
+#include <sys/random.h>
+
+#include <cerrno>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rclone_crypt_gpu.h"
+
+namespace rc {
+bool scrypt(const uint8_t* pw, size_t pwlen, const uint8_t* salt, size_t slen, uint64_t N, int r, int p,
+            uint8_t* out, size_t olen);
+}
+
+namespace {
+
+constexpr int64_t kBlockData = XS_BLOCK_DATA;
+constexpr int64_t kBlockHdr = XS_BLOCK_HDR;
+constexpr int64_t kBlockSize = XS_BLOCK_SIZE;
+constexpr int64_t kFileHdr = XS_FILE_HDR;
+const uint8_t kMagic[8] = {'R', 'C', 'L', 'O', 'N', 'E', 0, 0};
+// defaultSalt cipher.go:59
+const uint8_t kDefaultSalt[16] = {0xA8, 0x0D, 0xF4, 0x3A, 0x8F, 0xBD, 0x03, 0x08,
+                                  0xA7, 0xCA, 0xB8, 0x3E, 0x58, 0x1F, 0x86, 0xB1};
+
+bool is_pending(int32_t e) { return e != RC_NIL && e != RC_EOF; }  // "err != nil && err != io.EOF"
+
+// readers.ReadFill (lib/readers/readfill.go:11)
+int64_t read_fill(const rc_reader& r, uint8_t* buf, int64_t len, int32_t* err) {
+  int64_t n = 0;
+  int32_t e = RC_NIL;
+  while (n < len && e == RC_NIL) {
+    int64_t nn = r.read(r.user, buf + n, len - n, &e);
+    if (nn < 0) nn = 0;
+    n += nn;
+  }
+  *err = e;
+  return n;
+}
+
+// ---------------------------------------------------------------- GPU engine (process-wide)
+std::mutex g_engine_mu;
+xs_engine* g_engine = nullptr;
+bool g_engine_failed = false;
+
+xs_engine* engine() {
+  std::lock_guard<std::mutex> g(g_engine_mu);
+  if (g_engine || g_engine_failed) return g_engine;
+  int dev = 0;
+  if (const char* s = getenv("RCLONE_AMD_DEVICE")) dev = atoi(s);
+  uint32_t batch = 256;
+  if (const char* s = getenv("RCLONE_AMD_ENGINE_BLOCKS")) batch = (uint32_t)atoi(s);
+  g_engine = xs_engine_create(dev, batch, 3);
+  if (!g_engine) g_engine_failed = true;
+  return g_engine;
+}
+
+struct PinnedBuf {
+  uint8_t* p = nullptr;
+  size_t n = 0;
+  bool ensure(size_t bytes) {
+    if (n >= bytes) return true;
+    xs_host_free(p);
+    p = (uint8_t*)xs_host_alloc(bytes);
+    n = p ? bytes : 0;
+    return p != nullptr;
+  }
+  void release() {
+    xs_host_free(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~PinnedBuf() { release(); }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------- Cipher
+struct rc_cipher {
+  uint8_t data_key[32] = {0};
+  uint8_t name_key[32] = {0};
+  uint8_t name_tweak[16] = {0};
+  bool pass_bad_blocks = false;
+  rc_reader rand{};  // c.cryptoRand; read == NULL -> OS random
+  uint32_t batch_blocks = 64;
+  std::mutex rand_mu;
+};
+
+extern "C" int32_t rc_cipher_key(rc_cipher* c, const char* password, const char* salt) {
+  if (!c) return RC_ERR_INVALID;
+  uint8_t key[80] = {0};
+  if (password && password[0]) {
+    const uint8_t* s = kDefaultSalt;
+    size_t sl = sizeof kDefaultSalt;
+    if (salt && salt[0]) {
+      s = (const uint8_t*)salt;
+      sl = strlen(salt);
+    }
+    if (!rc::scrypt((const uint8_t*)password, strlen(password), s, sl, 16384, 8, 1, key, sizeof key))
+      return RC_ERR_INVALID;
+  }
+  memcpy(c->data_key, key, 32);
+  memcpy(c->name_key, key + 32, 32);
+  memcpy(c->name_tweak, key + 64, 16);
+  return RC_NIL;
+}
+
+extern "C" rc_cipher* rc_cipher_new(const char* password, const char* salt, int32_t* err) {
+  rc_cipher* c = new rc_cipher();
+  int32_t e = rc_cipher_key(c, password, salt);
+  if (err) *err = e;
+  if (e != RC_NIL) {
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
+extern "C" void rc_cipher_keys(const rc_cipher* c, uint8_t data_key[32], uint8_t name_key[32], uint8_t name_tweak[16]) {
+  if (data_key) memcpy(data_key, c->data_key, 32);
+  if (name_key) memcpy(name_key, c->name_key, 32);
+  if (name_tweak) memcpy(name_tweak, c->name_tweak, 16);
+}
+
+extern "C" void rc_cipher_set_pass_bad_blocks(rc_cipher* c, int32_t pass) { c->pass_bad_blocks = pass != 0; }
+extern "C" void rc_cipher_set_rand(rc_cipher* c, rc_reader rand) { c->rand = rand; }
+extern "C" void rc_cipher_set_batch_blocks(rc_cipher* c, uint32_t blocks) { c->batch_blocks = blocks ? blocks : 1; }
+extern "C" void rc_cipher_free(rc_cipher* c) { delete c; }
+
+// ---------------------------------------------------------------- sizes, nonce arithmetic
+extern "C" int64_t rc_encrypted_size(int64_t size) {
+  int64_t blocks = size / kBlockData, residue = size % kBlockData;
+  int64_t e = kFileHdr + blocks * kBlockSize;
+  if (residue != 0) e += kBlockHdr + residue;
+  return e;
+}
+
+extern "C" int64_t rc_decrypted_size(int64_t size, int32_t* err) {
+  if (err) *err = RC_NIL;
+  size -= kFileHdr;
+  if (size < 0) {
+    if (err) *err = RC_ERR_FILE_TOO_SHORT;
+    return 0;
+  }
+  int64_t blocks = size / kBlockSize, residue = size % kBlockSize;
+  int64_t d = blocks * kBlockData;
+  if (residue != 0) {
+    residue -= kBlockHdr;
+    if (residue <= 0) {
+      if (err) *err = RC_ERR_FILE_BAD_HEADER;
+      return 0;
+    }
+  }
+  return d + residue;
+}
+
+extern "C" void rc_calculate_underlying(int64_t offset, int64_t limit, int64_t out[4]) {
+  int64_t blocks = offset / kBlockData, discard = offset % kBlockData;
+  int64_t uoff = kFileHdr + blocks * kBlockSize;
+  int64_t ulim = -1;
+  if (limit >= 0) {
+    int64_t bytes_to_read = limit - (kBlockData - discard);
+    int64_t blocks_to_read = 1;
+    if (bytes_to_read > 0) {
+      int64_t extra = bytes_to_read / kBlockData, end = bytes_to_read % kBlockData;
+      if (end != 0) extra++;
+      blocks_to_read += extra;
+    }
+    ulim = blocks_to_read * kBlockSize;
+  }
+  out[0] = uoff;
+  out[1] = ulim;
+  out[2] = discard;
+  out[3] = blocks;
+}
+
+static void nonce_carry(uint8_t n[24], int i) {
+  for (; i < 24; i++) {
+    uint8_t digit = n[i];
+    uint8_t nd = (uint8_t)(digit + 1);
+    n[i] = nd;
+    if (nd >= digit) break;
+  }
+}
+extern "C" void rc_nonce_increment(uint8_t n[24]) { nonce_carry(n, 0); }
+extern "C" void rc_nonce_add(uint8_t n[24], uint64_t x) {
+  uint16_t carry = 0;
+  for (int i = 0; i < 8; i++) {
+    uint8_t digit = n[i];
+    uint8_t xd = (uint8_t)x;
+    x >>= 8;
+    carry = (uint16_t)(carry + digit + xd);
+    n[i] = (uint8_t)carry;
+    carry >>= 8;
+  }
+  if (carry != 0) nonce_carry(n, 8);
+}
+
+extern "C" const char* rc_error_string(int32_t e) {
+  switch (e) {
+    case RC_NIL: return "";
+    case RC_EOF: return "EOF";
+    case RC_UNEXPECTED_EOF: return "unexpected EOF";
+    case RC_ERR_FILE_TOO_SHORT: return "file is too short to be encrypted";
+    case RC_ERR_FILE_BAD_HEADER: return "file has truncated block header";
+    case RC_ERR_BAD_MAGIC: return "not an encrypted file - bad magic string";
+    case RC_ERR_BAD_BLOCK: return "failed to authenticate decrypted block - bad password?";
+    case RC_ERR_FILE_CLOSED: return "file already closed";
+    case RC_ERR_BAD_SEEK: return "Seek beyond end of file";
+    case RC_ERR_SHORT_NONCE: return "short read of nonce";
+    case RC_ERR_SEEK_NOT_INIT: return "can't seek - not initialised with newDecrypterSeek";
+    case RC_ERR_SEEK_WHENCE: return "can only seek from the start";
+    case RC_ERR_REOPEN: return "couldn't reopen file with offset and limit";
+    case RC_ERR_GPU: return "GPU crypt engine failure";
+    case RC_ERR_INVALID: return "invalid argument";
+    default: return "reader error";
+  }
+}
+
+// ---------------------------------------------------------------- encrypter
+struct rc_encrypter {
+  std::mutex mu;
+  rc_reader in{};
+  rc_cipher* c = nullptr;
+  uint8_t nonce[24] = {0};  // fh.nonce: initial nonce + blocks sealed
+  PinnedBuf plain, wire;    // staging (fh.readBuf / fh.buf)
+  int64_t buf_index = 0, buf_size = 0;
+  int32_t err = RC_NIL;
+  bool finished = false;
+};
+
+// finish (cipher.go:748-758)
+static int64_t enc_finish(rc_encrypter* fh, int32_t err, int32_t* out_err) {
+  if (fh->finished) {
+    *out_err = fh->err;
+    return 0;
+  }
+  fh->finished = true;
+  fh->err = err;
+  fh->plain.release();
+  fh->wire.release();
+  *out_err = err;
+  return 0;
+}
+
+extern "C" rc_encrypter* rc_encrypt_data(rc_cipher* c, rc_reader in, const uint8_t* nonce, int32_t* err) {
+  if (err) *err = RC_NIL;
+  if (!c || !in.read) {
+    if (err) *err = RC_ERR_INVALID;
+    return nullptr;
+  }
+  rc_encrypter* fh = new rc_encrypter();
+  fh->in = in;
+  fh->c = c;
+  if (nonce) {
+    memcpy(fh->nonce, nonce, 24);
+  } else {
+    // nonce.fromReader(c.cryptoRand) (cipher.go:630-636)
+    int32_t e = RC_NIL;
+    int64_t got = 0;
+    if (c->rand.read) {
+      std::lock_guard<std::mutex> g(c->rand_mu);
+      got = read_fill(c->rand, fh->nonce, 24, &e);
+    } else {
+      got = getrandom(fh->nonce, 24, 0);
+      e = got == 24 ? RC_NIL : RC_UNEXPECTED_EOF;
+    }
+    if (got != 24) {
+      if (err) *err = RC_ERR_SHORT_NONCE;
+      delete fh;
+      return nullptr;
+    }
+  }
+  const uint32_t batch = c->batch_blocks;
+  if (!fh->plain.ensure((size_t)batch * kBlockData) || !fh->wire.ensure((size_t)batch * kBlockSize + kFileHdr)) {
+    if (err) *err = RC_ERR_GPU;
+    delete fh;
+    return nullptr;
+  }
+  memcpy(fh->wire.p, kMagic, 8);
+  memcpy(fh->wire.p + 8, fh->nonce, 24);
+  fh->buf_size = kFileHdr;
+  return fh;
+}
+
+extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, int32_t* err) {
+  std::lock_guard<std::mutex> g(fh->mu);
+  *err = RC_NIL;
+  if (fh->finished) {
+    *err = fh->err;
+    return 0;
+  }
+  if (fh->buf_index >= fh->buf_size) {
+    // refill: ReadFill block by block exactly as encrypter.Read would, up to batch blocks
+    const uint32_t batch = fh->c->batch_blocks;
+    int64_t total = 0;
+    uint32_t nb = 0;
+    int32_t first_err = RC_NIL;
+    for (; nb < batch; nb++) {
+      int32_t e = RC_NIL;
+      int64_t got = read_fill(fh->in, fh->plain.p + (int64_t)nb * kBlockData, kBlockData, &e);
+      if (got == 0) {
+        if (nb == 0) first_err = e;
+        break;
+      }
+      total += got;
+      if (got < kBlockData || e != RC_NIL) {  // the next ReadFill must be a fresh call
+        nb++;
+        break;
+      }
+    }
+    if (nb == 0) return enc_finish(fh, first_err, err);
+    xs_engine* eng = engine();
+    if (!eng || xs_engine_seal(eng, fh->c->data_key, fh->nonce, 0, fh->plain.p, (uint64_t)total, fh->wire.p) != XS_OK)
+      return enc_finish(fh, RC_ERR_GPU, err);
+    fh->buf_index = 0;
+    fh->buf_size = total + (int64_t)nb * kBlockHdr;
+    rc_nonce_add(fh->nonce, nb);  // nonce.increment() once per sealed block
+  }
+  int64_t m = fh->buf_size - fh->buf_index;
+  if (m > n) m = n;
+  memcpy(p, fh->wire.p + fh->buf_index, (size_t)m);
+  fh->buf_index += m;
+  return m;
+}
+
+extern "C" void rc_encrypter_nonce(const rc_encrypter* fh, uint8_t out[24]) { memcpy(out, fh->nonce, 24); }
+extern "C" void rc_encrypter_free(rc_encrypter* fh) { delete fh; }
+
+// ---------------------------------------------------------------- decrypter
+struct rc_decrypter {
+  std::mutex mu;
+  rc_reader rc{};
+  bool have_rc = false;
+  uint8_t nonce[24] = {0};
+  uint8_t initial_nonce[24] = {0};
+  rc_cipher* c = nullptr;
+  PinnedBuf wire, plain, okb;
+  // decoded batch: blocks [cur, nblk) still to serve; block i has payload length blen[i]
+  std::vector<int64_t> blen;
+  std::vector<int32_t> berr;  // error returned by the ReadFill that produced block i
+  size_t cur = 0, nblk = 0;
+  int32_t tail_err = RC_NIL;  // what fillBuffer returns after the decoded blocks (RC_NIL = read more)
+  bool have_tail = false;
+  int64_t buf_index = 0, buf_size = 0;  // within the current block
+  int64_t cur_off = 0;                  // plaintext offset of the current block in plain
+  int32_t err = RC_NIL;
+  bool finished = false;
+  int64_t limit = -1;
+  rc_open_fn open = nullptr;
+  void* open_user = nullptr;
+  int32_t wrapped = RC_NIL;
+};
+
+static bool dec_alloc(rc_decrypter* fh) {
+  const uint32_t batch = fh->c->batch_blocks;
+  return fh->wire.ensure((size_t)batch * kBlockSize) && fh->plain.ensure((size_t)batch * kBlockData) &&
+         fh->okb.ensure(batch);
+}
+
+// finish (cipher.go:1042-1052): sets the sticky error and returns it
+static int32_t dec_finish(rc_decrypter* fh, int32_t err) {
+  if (fh->finished) return fh->err;
+  fh->finished = true;
+  fh->err = err;
+  fh->wire.release();
+  fh->plain.release();
+  fh->okb.release();
+  fh->nblk = fh->cur = 0;
+  fh->have_tail = false;
+  return err;
+}
+
+// unFinish (cipher.go:1054-1066)
+static bool dec_unfinish(rc_decrypter* fh) {
+  fh->finished = false;
+  fh->err = RC_NIL;
+  fh->buf_index = fh->buf_size = 0;
+  fh->nblk = fh->cur = 0;
+  fh->have_tail = false;
+  return dec_alloc(fh);
+}
+
+static int32_t dec_close_locked(rc_decrypter* fh) {
+  if (fh->finished && fh->err == RC_ERR_FILE_CLOSED) return RC_ERR_FILE_CLOSED;
+  if (!fh->finished) dec_finish(fh, RC_EOF);
+  fh->err = RC_ERR_FILE_CLOSED;
+  if (!fh->have_rc) return RC_NIL;
+  return fh->rc.close ? fh->rc.close(fh->rc.user) : RC_NIL;
+}
+
+// Read up to `want` blocks with the reference's per-block ReadFill sequence and open them on
+// the GPU.  Errors are not returned here; they are queued at the block position where
+// fillBuffer (cipher.go:862-898) would return them.
+static int32_t dec_read_batch(rc_decrypter* fh, uint32_t want) {
+  const uint32_t batch = fh->c->batch_blocks;
+  if (want == 0 || want > batch) want = batch;
+  fh->blen.assign(want, 0);
+  fh->berr.assign(want, RC_NIL);
+  fh->nblk = fh->cur = 0;
+  fh->have_tail = false;
+  int64_t total = 0;
+  uint32_t nb = 0;
+  for (; nb < want; nb++) {
+    int32_t e = RC_NIL;
+    int64_t got = read_fill(fh->rc, fh->wire.p + (int64_t)nb * kBlockSize, kBlockSize, &e);
+    if (got == 0) {
+      fh->have_tail = true;
+      fh->tail_err = e;
+      break;
+    }
+    if (got <= kBlockHdr) {  // "Check header + 1 byte exists"
+      fh->have_tail = true;
+      fh->tail_err = is_pending(e) ? e : RC_ERR_FILE_BAD_HEADER;
+      break;
+    }
+    fh->blen[nb] = got - kBlockHdr;
+    fh->berr[nb] = e;
+    total += got;
+    if (got < kBlockSize || e != RC_NIL) {
+      nb++;
+      break;
+    }
+  }
+  fh->nblk = nb;
+  if (nb == 0) return RC_NIL;
+  xs_engine* eng = engine();
+  if (!eng || xs_engine_open(eng, fh->c->data_key, fh->nonce, 0, fh->wire.p, (uint64_t)total, fh->plain.p,
+                             fh->okb.p) != XS_OK) {
+    fh->nblk = 0;
+    return RC_ERR_GPU;
+  }
+  return RC_NIL;
+}
+
+// fillBuffer (cipher.go:862-898): make the next block current.  Returns RC_NIL or the error
+// the reference returns at this position.
+static int32_t dec_fill(rc_decrypter* fh) {
+  if (fh->cur >= fh->nblk) {
+    if (fh->have_tail) {
+      fh->have_tail = false;
+      return fh->tail_err;
+    }
+    uint32_t want = 0;
+    if (fh->limit >= 0) want = (uint32_t)((fh->limit + kBlockData - 1) / kBlockData);
+    int32_t e = dec_read_batch(fh, want);  // want == 0: a full batch
+    if (e != RC_NIL) return e;
+    if (fh->nblk == 0) {
+      fh->have_tail = false;
+      return fh->tail_err;
+    }
+  }
+  const size_t i = fh->cur;
+  if (!fh->okb.p[i]) {
+    if (is_pending(fh->berr[i])) return fh->berr[i];  // pending error is likely more accurate
+    if (!fh->c->pass_bad_blocks) return RC_ERR_BAD_BLOCK;
+    // pass_bad_blocks: the kernel already zero-filled the block ("crypt: ignoring: ...")
+  }
+  fh->cur_off = (int64_t)i * kBlockData;
+  fh->buf_index = 0;
+  fh->buf_size = fh->blen[i];
+  fh->cur++;
+  rc_nonce_increment(fh->nonce);
+  return RC_NIL;
+}
+
+static rc_decrypter* new_decrypter(rc_cipher* c, rc_reader rc, int32_t* err) {
+  rc_decrypter* fh = new rc_decrypter();
+  fh->rc = rc;
+  fh->have_rc = true;
+  fh->c = c;
+  if (!dec_alloc(fh)) {
+    *err = RC_ERR_GPU;
+    dec_close_locked(fh);
+    delete fh;
+    return nullptr;
+  }
+  uint8_t hdr[kFileHdr];
+  int32_t e = RC_NIL;
+  int64_t n = read_fill(fh->rc, hdr, kFileHdr, &e);
+  int32_t fail = RC_NIL;
+  if (n < kFileHdr && e == RC_EOF) fail = RC_ERR_FILE_TOO_SHORT;
+  else if (e != RC_EOF && e != RC_NIL) fail = e;
+  else if (memcmp(hdr, kMagic, 8) != 0) fail = RC_ERR_BAD_MAGIC;
+  if (fail != RC_NIL) {
+    // finishAndClose (cipher.go:1089-1095)
+    dec_finish(fh, fail);
+    dec_close_locked(fh);
+    delete fh;
+    *err = fail;
+    return nullptr;
+  }
+  memcpy(fh->nonce, hdr + 8, 24);
+  memcpy(fh->initial_nonce, hdr + 8, 24);
+  *err = RC_NIL;
+  return fh;
+}
+
+extern "C" rc_decrypter* rc_decrypt_data(rc_cipher* c, rc_reader rc, int32_t* err) {
+  int32_t e = RC_NIL;
+  if (!c || !rc.read) {
+    if (err) *err = RC_ERR_INVALID;
+    return nullptr;
+  }
+  rc_decrypter* fh = new_decrypter(c, rc, &e);
+  if (err) *err = e;
+  return fh;
+}
+
+static int64_t range_seek_locked(rc_decrypter* fh, int64_t offset, int32_t whence, int64_t limit, int32_t* err);
+
+extern "C" rc_decrypter* rc_decrypt_data_seek(rc_cipher* c, rc_open_fn open, void* open_user, int64_t offset,
+                                              int64_t limit, int32_t* err) {
+  if (!c || !open) {
+    if (err) *err = RC_ERR_INVALID;
+    return nullptr;
+  }
+  rc_reader rc{};
+  bool do_range_seek = false, set_limit = false;
+  int32_t e;
+  if (offset == 0 && limit < 0) {
+    e = open(open_user, 0, -1, &rc);
+  } else if (offset == 0) {
+    int64_t u[4];
+    rc_calculate_underlying(offset, limit, u);
+    e = open(open_user, 0, kFileHdr + u[1], &rc);
+    set_limit = true;
+  } else {
+    e = open(open_user, 0, kFileHdr, &rc);
+    do_range_seek = true;
+  }
+  if (e != RC_NIL) {
+    if (err) *err = e;
+    return nullptr;
+  }
+  rc_decrypter* fh = new_decrypter(c, rc, &e);
+  if (!fh) {
+    if (err) *err = e;
+    return nullptr;
+  }
+  fh->open = open;
+  fh->open_user = open_user;
+  if (do_range_seek) {  // the handle is not shared yet: no lock needed
+    int32_t se = RC_NIL;
+    range_seek_locked(fh, offset, 0, limit, &se);
+    if (se != RC_NIL) {
+      dec_close_locked(fh);  // fh.Close()
+      delete fh;
+      if (err) *err = se;
+      return nullptr;
+    }
+  }
+  if (set_limit) fh->limit = limit;
+  if (err) *err = RC_NIL;
+  return fh;
+}
+
+extern "C" int64_t rc_decrypter_read(rc_decrypter* fh, uint8_t* p, int64_t n, int32_t* err) {
+  std::lock_guard<std::mutex> g(fh->mu);
+  *err = RC_NIL;
+  if (fh->finished) {
+    *err = fh->err;
+    return 0;
+  }
+  if (fh->buf_index >= fh->buf_size) {
+    int32_t e = dec_fill(fh);
+    if (e != RC_NIL) {
+      *err = dec_finish(fh, e);
+      return 0;
+    }
+  }
+  int64_t to_copy = fh->buf_size - fh->buf_index;
+  if (fh->limit >= 0 && fh->limit < to_copy) to_copy = fh->limit;
+  if (to_copy > n) to_copy = n;
+  memcpy(p, fh->plain.p + fh->cur_off + fh->buf_index, (size_t)to_copy);
+  fh->buf_index += to_copy;
+  if (fh->limit >= 0) {
+    fh->limit -= to_copy;
+    if (fh->limit == 0) {
+      *err = dec_finish(fh, RC_EOF);
+      return to_copy;
+    }
+  }
+  return to_copy;
+}
+
+// RangeSeek (cipher.go:972-1034)
+static int64_t range_seek_locked(rc_decrypter* fh, int64_t offset, int32_t whence, int64_t limit, int32_t* err) {
+  *err = RC_NIL;
+  if (!fh->open) {
+    *err = dec_finish(fh, RC_ERR_SEEK_NOT_INIT);
+    return 0;
+  }
+  if (whence != 0) {
+    *err = dec_finish(fh, RC_ERR_SEEK_WHENCE);
+    return 0;
+  }
+  if (fh->finished && fh->err == RC_EOF) {
+    if (!dec_unfinish(fh)) {
+      *err = dec_finish(fh, RC_ERR_GPU);
+      return 0;
+    }
+  } else if (fh->finished) {
+    *err = fh->err;
+    return 0;
+  }
+  int64_t u[4];
+  rc_calculate_underlying(offset, limit, u);
+  const int64_t uoff = u[0], ulim = u[1], discard = u[2], blocks = u[3];
+  memcpy(fh->nonce, fh->initial_nonce, 24);
+  rc_nonce_add(fh->nonce, (uint64_t)blocks);
+  // drop read-ahead
+  fh->nblk = fh->cur = 0;
+  fh->have_tail = false;
+  fh->buf_index = fh->buf_size = 0;
+  if (fh->have_rc && fh->rc.range_seek) {
+    int32_t e = fh->rc.range_seek(fh->rc.user, uoff, 0, ulim);
+    if (e != RC_NIL) {
+      *err = dec_finish(fh, e);
+      return 0;
+    }
+  } else {
+    if (fh->have_rc && fh->rc.close) (void)fh->rc.close(fh->rc.user);
+    fh->have_rc = false;
+    rc_reader nrc{};
+    int32_t e = fh->open(fh->open_user, uoff, ulim, &nrc);
+    if (e != RC_NIL) {
+      fh->wrapped = e;
+      *err = dec_finish(fh, RC_ERR_REOPEN);
+      return 0;
+    }
+    fh->rc = nrc;
+    fh->have_rc = true;
+  }
+  // fillBuffer for the first block; read ahead only what (discard + limit) needs
+  fh->limit = (limit >= 0) ? discard + limit : -1;
+  int32_t e = dec_fill(fh);
+  if (e != RC_NIL) {
+    *err = dec_finish(fh, e);
+    return 0;
+  }
+  if (discard > fh->buf_size) {
+    *err = dec_finish(fh, RC_ERR_BAD_SEEK);
+    return 0;
+  }
+  fh->buf_index = discard;
+  fh->limit = limit;
+  return offset;
+}
+
+extern "C" int64_t rc_decrypter_range_seek(rc_decrypter* fh, int64_t offset, int32_t whence, int64_t limit,
+                                           int32_t* err) {
+  std::lock_guard<std::mutex> g(fh->mu);
+  return range_seek_locked(fh, offset, whence, limit, err);
+}
+
+extern "C" int32_t rc_decrypter_close(rc_decrypter* fh) {
+  std::lock_guard<std::mutex> g(fh->mu);
+  return dec_close_locked(fh);
+}
+
+extern "C" void rc_decrypter_nonce(const rc_decrypter* fh, uint8_t out[24]) { memcpy(out, fh->nonce, 24); }
+extern "C" int32_t rc_decrypter_wrapped_error(const rc_decrypter* fh) { return fh->wrapped; }
+extern "C" void rc_decrypter_free(rc_decrypter* fh) { delete fh; }

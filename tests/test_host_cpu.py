@@ -1,0 +1,78 @@
+"""CPU-only checks of the native library (no GPU compute): the C ABI exports every symbol
+include/rclone_crypt_gpu.h declares, and the host logic of the cipher.go mirror (sizes,
+calculateUnderlying, nonce arithmetic, scrypt key derivation, error strings) against the
+reference's own tables (tests/golden/reference_kat.json, from backend/crypt/cipher_test.go).
+"""
+import os
+import re
+
+import pytest
+
+from rclone_amd import _lib, crypt
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "rclone_crypt_gpu.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = set(re.findall(r"\b((?:xs|rc)_[a-z0-9_]+)\s*\(", src))
+    return sorted(n for n in names if not n.endswith("_fn"))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 40
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(syms) <= set(_lib.SYMBOLS) | {"xs_engine_create"}
+
+
+def test_version_and_devices():
+    lib = _lib.lib()
+    assert b"gfx950" in lib.xs_version()
+    assert lib.xs_device_count() >= 0
+
+
+def test_encrypted_decrypted_size(ref_kat):
+    for n, e in ref_kat["encrypted_size"]:
+        assert crypt.encrypted_size(n) == e
+        assert crypt.decrypted_size(e) == n
+    for n, name in ref_kat["decrypted_size_errors"]:
+        with pytest.raises(getattr(crypt, name)):
+            crypt.decrypted_size(n)
+
+
+def test_calculate_underlying(ref_kat):
+    for off, lim, woff, wlim, wdisc, wblocks in ref_kat["calculate_underlying"]:
+        assert crypt.calculate_underlying(off, lim) == (woff, wlim, wdisc, wblocks)
+
+
+def test_nonce_increment_add(ref_kat):
+    for row in ref_kat["nonce_increment"]:
+        assert crypt.nonce_increment(bytes.fromhex(row["in"])).hex() == row["out"]
+    for row in ref_kat["nonce_add"]:
+        assert crypt.nonce_add(bytes.fromhex(row["in"]), row["add"]).hex() == row["out"]
+
+
+def test_key(ref_kat):
+    # TestKey cipher_test.go:1609-1642
+    c = crypt.Cipher()
+    assert c.data_key == bytes(32) and c.name_key == bytes(32) and c.name_tweak == bytes(16)
+    for kat in ref_kat["key_kat"]:
+        c.key(kat["password"], kat["salt"])
+        assert c.data_key.hex() == kat["dataKey"]
+        assert c.name_key.hex() == kat["nameKey"]
+        assert c.name_tweak.hex() == kat["nameTweak"]
+    c.key("", "")
+    assert c.data_key == bytes(32)
+
+
+def test_error_strings():
+    lib = _lib.lib()
+    assert lib.rc_error_string(-104) == b"failed to authenticate decrypted block - bad password?"
+    assert lib.rc_error_string(-101) == b"file is too short to be encrypted"
+    assert lib.rc_error_string(-106) == b"Seek beyond end of file"
+    assert str(crypt.ErrorEncryptedBadMagic(crypt.ErrorEncryptedBadMagic.message)) == \
+        "not an encrypted file - bad magic string"
