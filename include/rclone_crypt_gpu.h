@@ -97,6 +97,10 @@ int xs_keygen_object_dev(int seal, const uint8_t key[32], const uint8_t nonce0[2
                          uint64_t len, void *d_workspace, void *stream);
 int xs_crypt_dev(int seal, const void *d_workspace, uint64_t nblocks, const void *d_src, void *d_dst,
                  uint8_t *d_ok, void *stream);
+/* Key-schedule half of xs_seal_batch_dev / xs_open_batch_dev (descriptor mode). */
+int xs_keygen_batch_dev(int seal, const uint8_t key[32], const xs_block_desc *d_desc, uint64_t nblocks,
+                        const void *d_src, uint64_t src_len, const void *d_dst, uint64_t dst_len,
+                        void *d_workspace, void *stream);
 /* Fill d with the SplitMix64 stream (word k = mix(seed + (k+1)*0x9E3779B97F4A7C15)). */
 int xs_fill_random_dev(void *d, uint64_t nbytes, uint64_t seed, void *stream);
 

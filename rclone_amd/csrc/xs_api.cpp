@@ -189,6 +189,24 @@ int xs_crypt_dev(int seal, const void* d_workspace, uint64_t nblocks, const void
   return XS_OK;
 }
 
+int xs_keygen_batch_dev(int seal, const uint8_t key[32], const xs_block_desc* d_desc, uint64_t nblocks,
+                        const void* d_src, uint64_t src_len, const void* d_dst, uint64_t dst_len, void* d_workspace,
+                        void* stream) {
+  if (!key || !d_desc || !d_src || !d_dst || !d_workspace || !aligned16(d_workspace)) {
+    set_error("xs_keygen_batch_dev: bad argument");
+    return XS_ERR_INVALID;
+  }
+  if (nblocks == 0) return XS_OK;
+  NonceArg bounds{};
+  bounds.n[0] = (uint32_t)src_len; bounds.n[1] = (uint32_t)(src_len >> 32);
+  bounds.n[2] = (uint32_t)dst_len; bounds.n[3] = (uint32_t)(dst_len >> 32);
+  bounds.n[4] = (uint32_t)((uintptr_t)d_src & 15u); bounds.n[5] = (uint32_t)((uintptr_t)d_dst & 15u);
+  hipError_t e = launch_keygen(seal ? 2 : 3, key_arg(key), bounds, 0, 0, nblocks, d_desc, (BlockKey*)d_workspace,
+                               (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "keygen launch");
+  return XS_OK;
+}
+
 int xs_fill_random_dev(void* d, uint64_t nbytes, uint64_t seed, void* stream) {
   if (!d || (nbytes & 7u) || !aligned16(d)) {
     set_error("xs_fill_random_dev: need a 16-byte aligned buffer and a multiple of 8 bytes");

@@ -1,0 +1,58 @@
+"""Multi-GPU partitioning of crypt blocks (one process per GPU, torch.distributed).
+
+Blocks are independent (block i of an object is a pure function of key, nonce0 + i and its
+plaintext, cipher.go:665-678), so an object set shards with no data-path exchange: rank r of
+W owns the blocks b with b % W == r (round-robin, BASELINE config 4).  Each rank seals its
+blocks through the descriptor entry point (per-block nonce = nonce0 + b), laid out
+contiguously in its own HBM.  The only collective is one all-reduce of a few int64 counters
+(blocks, bytes, tag failures) -- RCCL over xGMI with backend "nccl", gloo on CPU.
+"""
+import numpy as np
+
+from ._lib import XsBlockDesc
+
+BLOCK_DATA = 65536
+BLOCK_SIZE = 65552
+
+
+def owned_blocks(total_blocks: int, world: int, rank: int) -> np.ndarray:
+    """Global indices of the blocks rank `rank` owns (round-robin)."""
+    if not (0 <= rank < world):
+        raise ValueError("bad rank")
+    return np.arange(rank, total_blocks, world, dtype=np.int64)
+
+
+def nonce_plus(nonce0: bytes, idx: np.ndarray) -> np.ndarray:
+    """nonce0 + idx as 24-byte little-endian numbers (nonce.add, cipher.go:665) -> (n, 24) u8."""
+    base = int.from_bytes(bytes(nonce0), "little")
+    out = np.empty((len(idx), 24), dtype=np.uint8)
+    for j, i in enumerate(idx.tolist()):
+        out[j] = np.frombuffer(((base + int(i)) % (1 << 192)).to_bytes(24, "little"), dtype=np.uint8)
+    return out
+
+
+def seal_descriptors(nonce0: bytes, global_idx: np.ndarray, block_len: int = BLOCK_DATA,
+                     open_mode: bool = False) -> np.ndarray:
+    """Descriptors for the given global blocks, packed contiguously in local buffers:
+    seal: plaintext at i*65536 -> wire block at i*65552; open: the reverse."""
+    n = len(global_idx)
+    d = np.zeros(n, dtype=np.dtype([("src", "<u8"), ("dst", "<u8"), ("len", "<u4"), ("res", "<u4"),
+                                    ("nonce", "u1", (24,))]))
+    assert d.dtype.itemsize == 48 and XsBlockDesc
+    i = np.arange(n, dtype=np.uint64)
+    if open_mode:
+        d["src"] = i * BLOCK_SIZE
+        d["dst"] = i * BLOCK_DATA
+    else:
+        d["src"] = i * BLOCK_DATA
+        d["dst"] = i * BLOCK_SIZE
+    d["len"] = block_len
+    d["nonce"] = nonce_plus(nonce0, global_idx)
+    return d
+
+
+def reduce_counters(counters, dist=None, group=None):
+    """Sum a small int64 tensor of counters over all ranks (the only collective)."""
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
+    return counters
