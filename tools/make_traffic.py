@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc.sh) into HBM bytes per
+xs_crypt launch: profiles/pmc_traffic.json (read by bench.py as roofline.traffic).
+
+Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE counts exactly half the
+bytes of a wide (16 B/lane) streaming read -- global_load and LDS-DMA alike -- so reads =
+2 x FETCH_SIZE; WRITE_SIZE is exact for 16 B/lane stores.  Both are in KiB."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import load  # noqa: E402
+
+
+def main():
+    d, out = sys.argv[1], sys.argv[2]
+    acc = load(d)
+    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE ({d}), reads x2 (gfx950 FETCH_SIZE halving)"}
+    for k, cs in acc.items():
+        for name, key in (("xs_crypt<true>", "seal"), ("xs_crypt<false>", "open")):
+            if name in k and "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+                fetch = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"]) * 1024 * 2
+                write = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) * 1024
+                res[f"{key}_read_bytes_per_launch"] = round(fetch)
+                res[f"{key}_write_bytes_per_launch"] = round(write)
+                res[f"{key}_bytes_per_launch"] = round(fetch + write)
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
