@@ -274,6 +274,88 @@ __device__ __forceinline__ void padd_part(P5& h, uint32_t w0, uint32_t w1, uint3
   h.v[4] += (w3 >> 8);
 }
 
+// ---------------------------------------------------------------- Poly1305, radix 2^32
+// For multiplications by the clamped key r itself (r1..r3 divisible by 4, all words < 2^28)
+// the 32-bit-word form needs 20 multiply-adds and no limb splitting (OpenSSL's 32-bit
+// poly1305_blocks): h = (h + c + 2^128) * r, partially reduced (h4 <= 4 on exit).
+struct P32 {
+  uint32_t w0, w1, w2, w3, w4;
+};
+struct RClamp {
+  uint32_t r0, r1, r2, r3, s1, s2, s3;  // s_i = r_i + r_i/4 = 5 r_i / 4
+};
+
+__device__ __forceinline__ void pstep32(P32& h, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, const RClamp& r) {
+  // h += c + 2^128 (32-bit add-with-carry chain)
+  unsigned cy;
+  const uint32_t h0 = __builtin_addc(h.w0, c0, 0u, &cy);
+  const uint32_t h1 = __builtin_addc(h.w1, c1, cy, &cy);
+  const uint32_t h2 = __builtin_addc(h.w2, c2, cy, &cy);
+  const uint32_t h3 = __builtin_addc(h.w3, c3, cy, &cy);
+  const uint32_t h4 = __builtin_addc(h.w4, 1u, cy, &cy);
+  // column sums (v_mad_u64_u32 chains)
+  const uint64_t d0 = (uint64_t)h0 * r.r0 + (uint64_t)h1 * r.s3 + (uint64_t)h2 * r.s2 + (uint64_t)h3 * r.s1;
+  const uint64_t d1 = (uint64_t)h0 * r.r1 + (uint64_t)h1 * r.r0 + (uint64_t)h2 * r.s3 + (uint64_t)h3 * r.s2 +
+                      (uint64_t)h4 * r.s1;
+  const uint64_t d2 = (uint64_t)h0 * r.r2 + (uint64_t)h1 * r.r1 + (uint64_t)h2 * r.r0 + (uint64_t)h3 * r.s3 +
+                      (uint64_t)h4 * r.s2;
+  const uint64_t d3 = (uint64_t)h0 * r.r3 + (uint64_t)h1 * r.r2 + (uint64_t)h2 * r.r1 + (uint64_t)h3 * r.r0 +
+                      (uint64_t)h4 * r.s3;
+  // carry the high words up: d_{i+1} += d_i >> 32
+  uint32_t l0 = (uint32_t)d0, l1 = (uint32_t)d1, l2 = (uint32_t)d2, l3 = (uint32_t)d3;
+  uint32_t u1 = (uint32_t)(d1 >> 32), u2 = (uint32_t)(d2 >> 32), u3 = (uint32_t)(d3 >> 32);
+  l1 = __builtin_addc(l1, (uint32_t)(d0 >> 32), 0u, &cy);
+  u1 = u1 + cy;
+  l2 = __builtin_addc(l2, u1, 0u, &cy);
+  u2 = u2 + cy;
+  l3 = __builtin_addc(l3, u2, 0u, &cy);
+  u3 = u3 + cy;
+  const uint32_t h4n = h4 * r.r0 + u3;
+  // fold bits >= 130: h += (h4n >> 2) * 5
+  const uint32_t c = (h4n >> 2) + (h4n & ~3u);
+  h.w0 = __builtin_addc(l0, c, 0u, &cy);
+  h.w1 = __builtin_addc(l1, 0u, cy, &cy);
+  h.w2 = __builtin_addc(l2, 0u, cy, &cy);
+  h.w3 = __builtin_addc(l3, 0u, cy, &cy);
+  h.w4 = (h4n & 3u) + cy;
+}
+
+// h += c + 2^128 in radix 2^32 (no multiply)
+__device__ __forceinline__ void padd32(P32& h, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+  unsigned cy;
+  h.w0 = __builtin_addc(h.w0, c0, 0u, &cy);
+  h.w1 = __builtin_addc(h.w1, c1, cy, &cy);
+  h.w2 = __builtin_addc(h.w2, c2, cy, &cy);
+  h.w3 = __builtin_addc(h.w3, c3, cy, &cy);
+  h.w4 = h.w4 + 1u + cy;
+}
+
+// radix 2^32 (w4 < 2^6) -> radix 2^26 limbs (limb 4 < 2^27), exact
+__device__ __forceinline__ P5 to26(const P32& h) {
+  P5 o;
+  o.v[0] = h.w0 & M26;
+  o.v[1] = alignbit(h.w1, h.w0, 26) & M26;
+  o.v[2] = alignbit(h.w2, h.w1, 20) & M26;
+  o.v[3] = alignbit(h.w3, h.w2, 14) & M26;
+  o.v[4] = alignbit(h.w4, h.w3, 8);
+  return o;
+}
+
+// radix 2^26 limbs (each < 2^27) -> radix 2^32, exact (additive repacking with carries)
+__device__ __forceinline__ P32 to32(const P5& o) {
+  P32 h;
+  uint64_t v = (uint64_t)o.v[0] + ((uint64_t)o.v[1] << 26);
+  h.w0 = (uint32_t)v;
+  v = (v >> 32) + ((uint64_t)o.v[2] << 20);
+  h.w1 = (uint32_t)v;
+  v = (v >> 32) + ((uint64_t)o.v[3] << 14);
+  h.w2 = (uint32_t)v;
+  v = (v >> 32) + ((uint64_t)o.v[4] << 8);
+  h.w3 = (uint32_t)v;
+  h.w4 = (uint32_t)(v >> 32);
+  return h;
+}
+
 // Carry-normalise limbs < 2^32 into limbs < 2^26 (+2^6 on limb 1), value mod p preserved.
 __device__ __forceinline__ void pnorm(P5& h) {
   uint32_t c;
@@ -483,6 +565,13 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
     RR.v[i] = bk->R[i];
   }
   const PMul Mr = pmul_prep(rr), MR = pmul_prep(RR);
+  RClamp rc;
+  {
+    const P32 r32 = to32(rr);
+    rc.r0 = r32.w0; rc.r1 = r32.w1; rc.r2 = r32.w2; rc.r3 = r32.w3;
+    rc.s1 = rc.r1 + (rc.r1 >> 2); rc.s2 = rc.r2 + (rc.r2 >> 2); rc.s3 = rc.r3 + (rc.r3 >> 2);
+  }
+  P32 h32 = {0, 0, 0, 0, 0};  // FULL path accumulator (radix 2^32)
   int c_last = -1;
   P5 t1, t2;
 
@@ -583,10 +672,14 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       if (FULL) {
-        padd_full(h, cw[4 * j], cw[4 * j + 1], cw[4 * j + 2], cw[4 * j + 3]);
-        h = pmul_u(h, (j == 3 && s < 3) ? MR : Mr);
+        if (j < 3 || s == 3) {
+          pstep32(h32, cw[4 * j], cw[4 * j + 1], cw[4 * j + 2], cw[4 * j + 3], rc);
+        } else {  // gap to the lane's next group: * r^1021 in radix 2^26
+          padd32(h32, cw[4 * j], cw[4 * j + 1], cw[4 * j + 2], cw[4 * j + 3]);
+          h32 = to32(pmul_u(to26(h32), MR));
+        }
         if (j == 1 && key_slots) {  // discard what lane 0 hashed for the key slots
-          h.v[0] = h.v[1] = h.v[2] = h.v[3] = h.v[4] = 0;
+          h32.w0 = h32.w1 = h32.w2 = h32.w3 = h32.w4 = 0;
         }
       } else {
         if (plen[j] != 0u) {
@@ -646,13 +739,17 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
       uint32_t cw[4];
 #pragma unroll
       for (int i = 0; i < 4; i++) cw[i] = SEAL ? o4[i] : w[i];
-      if (L == 16u) {
-        padd_full(h, cw[0], cw[1], cw[2], cw[3]);
+      if (FULL) {
+        pstep32(h32, cw[0], cw[1], cw[2], cw[3], rc);
       } else {
-        cw[L >> 2] |= 1u << (8u * (L & 3u));
-        padd_part(h, cw[0], cw[1], cw[2], cw[3]);
+        if (L == 16u) {
+          padd_full(h, cw[0], cw[1], cw[2], cw[3]);
+        } else {
+          cw[L >> 2] |= 1u << (8u * (L & 3u));
+          padd_part(h, cw[0], cw[1], cw[2], cw[3]);
+        }
+        h = pmul_u(h, Mr);
       }
-      h = pmul_u(h, Mr);
       c_last = c;
     }
   }
@@ -668,7 +765,7 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
       h = pmul(h, pmul(t1, t2));
     }
   } else {
-    h = pmul(h, pmul(t1, t2));
+    h = pmul(to26(h32), pmul(t1, t2));
   }
 }
 
