@@ -14,7 +14,7 @@ struct NonceArg {
   uint32_t n[6];
 };
 
-// Per-block key schedule written by xs_keygen, read by xs_crypt (1440 bytes).
+// Per-block key schedule written by xs_keygen, read by xs_crypt (960 bytes).
 struct __attribute__((aligned(16))) BlockKey {
   uint32_t subkey[8];  // HSalsa20(key, nonce[0:16])
   uint32_t n2[2];      // nonce[16:24] (Salsa20 words 6, 7)
@@ -25,12 +25,12 @@ struct __attribute__((aligned(16))) BlockKey {
   uint32_t s[4];       // Poly1305 s
   uint32_t ks1024[8];  // keystream block 1024 words 0..7 (message chunks 4094, 4095)
   uint32_t r[5];       // clamped r, radix 2^26
-  uint32_t R[5];       // r^1021 (gap between a lane's chunk groups)
+  uint32_t R[5];       // r^253 (gap between a lane's chunk groups)
   uint32_t pad[2];
   uint32_t T1[32][5];  // r^0 .. r^31
-  uint32_t T2[32][5];  // r^(32a), a = 0..31
+  uint32_t T2[8][5];   // r^(32a), a = 0..7 (a lane's final exponent is < 256)
 };
-static_assert(sizeof(BlockKey) == 1440, "BlockKey layout");
+static_assert(sizeof(BlockKey) == 960, "BlockKey layout");
 
 hipError_t launch_keygen(int mode, const KeyArg& key, const NonceArg& nonce0, uint64_t first_block,
                          uint64_t total_len, uint64_t nblocks, const xs_block_desc* desc, BlockKey* out,

@@ -8,16 +8,16 @@
 //   xs_keygen  one lane per crypt block: per-block nonce, HSalsa20 subkey, keystream
 //              block 0 (Poly1305 key r||s), keystream block 1024 words 0..7 (the last
 //              two 16-byte chunks of a full block) and the Poly1305 power tables the
-//              main kernel needs (r, r^1021, r^0..31, r^(32a)).  ~0.5% of the work.
-//   xs_crypt   one 64 KiB block per 256-lane workgroup (4 wave64s).  Lane t owns the
-//              Salsa20 keystream blocks K = t + 256*s (s = 0..3), i.e. message chunks
+//              main kernel needs (r, r^253, r^0..31, r^(32a)).  ~2% of the work.
+//   xs_crypt   one 64 KiB block per wave64 (four per 256-lane workgroup).  Lane l owns the
+//              Salsa20 keystream blocks K = l + 64*s (s = 0..15), i.e. message chunks
 //              4K-2 .. 4K+1 (16 bytes each, offset by the 32-byte Poly1305 key).  A lane
 //              keeps the whole 16-word Salsa20 state in VGPRs; key/nonce words are
 //              wave-uniform and live in SGPRs.  Each lane runs a strided Horner over its
-//              own chunks with uniform multipliers r (inside a group) and r^1021 (between
+//              own chunks with uniform multipliers r (inside a group) and r^253 (between
 //              groups), then multiplies by r^e (e = chunks after its last one) from the
-//              tables; the 256 partial sums are added with wave shuffles + LDS and lane 0
-//              adds s and writes (seal) or checks (open) the tag.
+//              tables; the 64 partial sums are added with wave shuffles and lane 0 adds s
+//              and writes (seal) or checks (open) the tag.
 //   Poly1305 arithmetic is radix 2^26 (5 limbs): the product columns are
 //   v_mad_u64_u32 chains, which measured as fast as v_alignbit on gfx950.
 //
@@ -510,20 +510,22 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
     for (int j = 0; j < 5; j++) o->T1[i][j] = p.v[j];
     if (i < 31) p = pcanon(pmul(p, r));
   }
-  P5 r31 = p;
   P5 r32 = pcanon(pmul(p, r));
   p.v[0] = 1; p.v[1] = 0; p.v[2] = 0; p.v[3] = 0; p.v[4] = 0;
-  for (int a = 0; a < 32; a++) {
+  for (int a = 0; a < 8; a++) {
 #pragma unroll
     for (int j = 0; j < 5; j++) o->T2[a][j] = p.v[j];
-    if (a < 31) p = pcanon(pmul(p, r32));
+    if (a < 7) p = pcanon(pmul(p, r32));
   }
-  // r^1021 = r^992 * r^29
-  P5 r29;
+  // r^253 = r^224 * r^29: the Horner gap between a lane's consecutive chunk groups
+  // (64 lanes per block, 4 chunks per group: 4*64 - 3)
+  P5 r29, r224;
 #pragma unroll
-  for (int j = 0; j < 5; j++) r29.v[j] = o->T1[29][j];
-  (void)r31;
-  P5 R = pcanon(pmul(p, r29));
+  for (int j = 0; j < 5; j++) {
+    r29.v[j] = o->T1[29][j];
+    r224.v[j] = o->T2[7][j];
+  }
+  P5 R = pcanon(pmul(r224, r29));
 #pragma unroll
   for (int i = 0; i < 5; i++) o->R[i] = R.v[i];
 }
@@ -533,13 +535,15 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
 // ok[blk] = 1 if the tag verified (else the plaintext is zero-filled, the
 // pass_bad_blocks contract of cipher.go:885-893).
 //
-// Per group s (s = 0..3) lane t owns keystream block K = t + 256 s and message chunks
-// 4K-2 .. 4K+1.  The wave's 4 KiB of input for the group is staged into its own LDS slot by
+// One 64 KiB block per wave64 (a 256-thread workgroup carries four blocks; no barriers).
+// Group s (s = 0..15): lane l owns keystream block K = l + 64 s and message chunks
+// 4K-2 .. 4K+1.  The wave's 4 KiB of input for the group is staged into its LDS slot by
 // global_load_lds_dwordx4 (no VGPRs held across the 20 Salsa20 rounds), read back after the
-// keystream is ready, XORed and stored.  Lane 255 also owns chunks 4094, 4095 (keystream
-// block 1024, precomputed by keygen), so every lane's Horner multipliers are uniform:
-// r inside a group, r^1021 between groups.
-constexpr int LDS_WORDS = 4 * 1024 + 32;
+// keystream is ready, XORed and stored.  Lane 63 also owns chunks 4094, 4095 (keystream block
+// 1024, precomputed by keygen), so every lane's Horner multipliers are uniform: r inside a
+// group, r^253 between groups.
+constexpr int LDS_WORDS = 4 * 1024;
+constexpr uint32_t LANES = 64, GROUPS = 16;
 typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ uint32_t keep_mask(uint32_t L, uint32_t i) {
@@ -549,9 +553,8 @@ __device__ __forceinline__ uint32_t keep_mask(uint32_t L, uint32_t i) {
 
 template <bool SEAL, bool FULL>
 __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, const uint8_t* __restrict__ pin,
-                                            uint8_t* __restrict__ pout, uint32_t n, uint32_t* lds, P5& h) {
-  const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-  uint32_t* wb = lds + wave * 1024u;  // this wave's 4 KiB staging slot
+                                            uint8_t* __restrict__ pout, uint32_t n, uint32_t* wb, P5& h) {
+  const uint32_t l = threadIdx.x & 63u;
   const int nc = FULL ? 4096 : (int)((n + 15u) >> 4);
   const int nfull = FULL ? 4096 : (int)(n >> 4);  // chunks that are whole 16-byte chunks
   uint32_t k[8];
@@ -576,8 +579,8 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
   P5 t1, t2;
 
 #pragma unroll 1
-  for (int s = 0; s < 4; s++) {
-    const uint32_t K = t + 256u * (uint32_t)s;
+  for (int s = 0; s < (int)GROUPS; s++) {
+    const uint32_t K = l + LANES * (uint32_t)s;
     const int cfirst = 4 * (int)K - 2;
     if (!FULL && cfirst >= nc) break;
     // stage this group's input (whole chunks only) into the wave's LDS slot
@@ -588,14 +591,12 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
       const bool whole = FULL ? (c >= 0) : (c >= 0 && c < nfull);
       if (whole) __builtin_amdgcn_global_load_lds(src + 16 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
     }
-    if (s == 3) {  // final-exponent tables, needed after the loop
-      const uint32_t e = FULL ? ((t == 255u) ? 0u : 1022u - 4u * t) : 0u;
-      if (FULL) {
+    if (FULL && s == (int)GROUPS - 1) {  // final-exponent tables, needed after the loop
+      const uint32_t e = (l == 63u) ? 0u : 254u - 4u * l;
 #pragma unroll
-        for (int i = 0; i < 5; i++) {
-          t1.v[i] = bk->T1[e & 31u][i];
-          t2.v[i] = bk->T2[e >> 5][i];
-        }
+      for (int i = 0; i < 5; i++) {
+        t1.v[i] = bk->T1[e & 31u][i];
+        t2.v[i] = bk->T2[e >> 5][i];
       }
     }
     uint32_t ks[16];
@@ -604,7 +605,7 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
     uint32_t d[16];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      uint4 v = *reinterpret_cast<const uint4*>(wb + 256 * j + 4 * lane);
+      uint4 v = *reinterpret_cast<const uint4*>(wb + 256 * j + 4 * l);
       d[4 * j] = v.x; d[4 * j + 1] = v.y; d[4 * j + 2] = v.z; d[4 * j + 3] = v.w;
     }
     uint32_t plen[4];  // bytes of each chunk (16 whole, 0 absent, else partial)
@@ -629,8 +630,6 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
           d[4 * j] = w[0]; d[4 * j + 1] = w[1]; d[4 * j + 2] = w[2]; d[4 * j + 3] = w[3];
         }
       }
-    }
-    if (!FULL) {
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         if (plen[j] == 0u) { d[4 * j] = 0; d[4 * j + 1] = 0; d[4 * j + 2] = 0; d[4 * j + 3] = 0; }
@@ -641,13 +640,8 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
     for (int i = 0; i < 16; i++) o[i] = d[i] ^ ks[i];
     if (!FULL) {
 #pragma unroll
-      for (int j = 0; j < 4; j++) {  // absent chunks hash as zero
+      for (int j = 0; j < 4; j++) {  // absent chunks hash as zero; partial chunks keep L bytes
         if (plen[j] == 0u) { o[4 * j] = 0; o[4 * j + 1] = 0; o[4 * j + 2] = 0; o[4 * j + 3] = 0; }
-      }
-    }
-    if (!FULL) {
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
         if (plen[j] != 16u) {
 #pragma unroll
           for (int i = 0; i < 4; i++) o[4 * j + i] &= keep_mask(plen[j], (uint32_t)i);
@@ -655,7 +649,7 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
       }
     }
     uint8_t* dst = pout + 64u * K - 32u;
-    const bool key_slots = FULL && s == 0 && t == 0u;  // chunks -2, -1 of K = 0: the Poly1305 key
+    const bool key_slots = FULL && s == 0 && l == 0u;  // chunks -2, -1 of K = 0: the Poly1305 key
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       if (FULL) {
@@ -663,18 +657,18 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
           *reinterpret_cast<uint4*>(dst + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
       } else if (plen[j] == 16u) {
         *reinterpret_cast<uint4*>(dst + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
-      } else if (!FULL && plen[j] != 0u) {
+      } else if (plen[j] != 0u) {
         for (uint32_t i = 0; i < plen[j]; i++) dst[16 * j + i] = (uint8_t)(o[4 * j + (i >> 2)] >> (8u * (i & 3u)));
       }
     }
-    // Poly1305 over the ciphertext: (h + c) * r within the group, * r^1021 (or r) at its end
+    // Poly1305 over the ciphertext: (h + c) * r within the group, * r^253 (or r) at its end
     const uint32_t* cw = SEAL ? o : d;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       if (FULL) {
-        if (j < 3 || s == 3) {
+        if (j < 3 || s == (int)GROUPS - 1) {
           pstep32(h32, cw[4 * j], cw[4 * j + 1], cw[4 * j + 2], cw[4 * j + 3], rc);
-        } else {  // gap to the lane's next group: * r^1021 in radix 2^26
+        } else {  // gap to the lane's next group: * r^253 in radix 2^26
           padd32(h32, cw[4 * j], cw[4 * j + 1], cw[4 * j + 2], cw[4 * j + 3]);
           h32 = to32(pmul_u(to26(h32), MR));
         }
@@ -699,7 +693,7 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
           h.v[2] += alignbit(w2, w1, 20) & M26;
           h.v[3] += alignbit(w3, w2, 14) & M26;
           h.v[4] += (w3 >> 8) | pad;
-          const bool use_R = (j == 3) && (s < 3) && (cfirst + 1024 < nc);
+          const bool use_R = (j == 3) && (s < (int)GROUPS - 1) && (cfirst + 4 * (int)LANES < nc);
           PMul M;
 #pragma unroll
           for (int i = 0; i < 5; i++) {
@@ -713,8 +707,8 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
     }
     if (FULL) c_last = cfirst + 3;
   }
-  // lane 255 owns chunks 4094, 4095 (keystream block 1024 words 0..7)
-  if (t == 255u && nc > 4094) {
+  // lane 63 owns chunks 4094, 4095 (keystream block 1024 words 0..7)
+  if (l == 63u && nc > 4094) {
 #pragma unroll 1
     for (int j = 0; j < 2; j++) {
       const int c = 4094 + j;
@@ -771,13 +765,18 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
 
 template <bool SEAL>
 __global__ void __launch_bounds__(256, XS_WAVES_PER_EU) xs_crypt(const BlockKey* __restrict__ keys,
+                                                                 uint64_t nblocks,
                                                                  const uint8_t* __restrict__ src,
                                                                  uint8_t* __restrict__ dst,
                                                                  uint8_t* __restrict__ ok) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
-  const BlockKey* bk = keys + blockIdx.x;
+  const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63u;
+  // wave-uniform block index
+  const uint64_t blk = (uint64_t)blockIdx.x * 4u + (uint64_t)__builtin_amdgcn_readfirstlane(wave);
+  if (blk >= nblocks) return;
+  const BlockKey* bk = keys + blk;
   if (bk->flags) {  // rejected descriptor: write nothing
-    if (!SEAL && threadIdx.x == 0) ok[blockIdx.x] = 0;
+    if (!SEAL && l == 0) ok[blk] = 0;
     return;
   }
   const uint32_t n = bk->len;
@@ -785,52 +784,41 @@ __global__ void __launch_bounds__(256, XS_WAVES_PER_EU) xs_crypt(const BlockKey*
   uint8_t* out = dst + bk->dst;
   const uint8_t* pin = SEAL ? in : in + XS_BLOCK_HDR;
   uint8_t* pout = SEAL ? out + XS_BLOCK_HDR : out;
-  const uint32_t t = threadIdx.x;
+  uint32_t* wb = lds + wave * 1024u;
 
   P5 h;
   h.v[0] = h.v[1] = h.v[2] = h.v[3] = h.v[4] = 0;
-  if (n == XS_BLOCK_DATA) crypt_block<SEAL, true>(bk, pin, pout, n, lds, h);
-#ifndef XS_ONLY_FULL
-  else crypt_block<SEAL, false>(bk, pin, pout, n, lds, h);
-#endif
+  if (n == XS_BLOCK_DATA) crypt_block<SEAL, true>(bk, pin, pout, n, wb, h);
+  else crypt_block<SEAL, false>(bk, pin, pout, n, wb, h);
 
-  // sum the 256 partials: wave shuffles, then LDS across the 4 waves
+  // sum the 64 partials with wave shuffles (limbs < 2^26+2^6 -> < 2^32 after 5 levels)
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
 #pragma unroll
     for (int i = 0; i < 5; i++) h.v[i] += (uint32_t)__shfl_xor((int)h.v[i], off, 64);
     if (off == 2) pnorm(h);
   }
-  uint32_t* red = lds + 4 * 1024;
-  const uint32_t wave = t >> 6, lane = t & 63u;
-  if (!SEAL) __builtin_amdgcn_s_waitcnt(0);  // our plaintext stores complete before a possible zero-fill
-  if (lane == 0) {
-#pragma unroll
-    for (int i = 0; i < 5; i++) red[wave * 5 + i] = h.v[i];
-  }
-  __syncthreads();
-  if (t == 0) {
-    P5 acc;
-#pragma unroll
-    for (int i = 0; i < 5; i++) acc.v[i] = red[i] + red[5 + i] + red[10 + i] + red[15 + i];
-    P5 hc = pcanon(acc);
+  uint32_t verdict = 1;
+  if (l == 0) {
+    P5 hc = pcanon(h);
     uint32_t s4[4] = {bk->s[0], bk->s[1], bk->s[2], bk->s[3]};
     uint32_t tag[4];
     ptag(hc, s4, tag);
     if (SEAL) {
       *reinterpret_cast<uint4*>(out) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
     } else {
-      uint4 want = *reinterpret_cast<const uint4*>(in);
-      uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) | (want.z ^ tag[2]) | (want.w ^ tag[3]);
-      red[20] = diff == 0 ? 1u : 0u;
-      ok[blockIdx.x] = diff == 0 ? 1 : 0;
+      const uint4 want = *reinterpret_cast<const uint4*>(in);
+      const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) | (want.z ^ tag[2]) | (want.w ^ tag[3]);
+      verdict = diff == 0 ? 1u : 0u;
+      ok[blk] = diff == 0 ? 1 : 0;
     }
   }
   if (!SEAL) {
-    __syncthreads();
-    if (red[20] == 0) {
-      // authentication failed: zero the block's plaintext (ordered after the stores above)
-      for (uint32_t off = 16u * t; off < n; off += 16u * 256u) {
+    verdict = (uint32_t)__shfl((int)verdict, 0, 64);
+    if (verdict == 0) {
+      // authentication failed: zero the block's plaintext, after our own stores completed
+      __builtin_amdgcn_s_waitcnt(0);
+      for (uint32_t off = 16u * l; off < n; off += 16u * LANES) {
         const uint32_t L = (n - off) < 16u ? (n - off) : 16u;
         if (L == 16u) *reinterpret_cast<uint4*>(pout + off) = make_uint4(0, 0, 0, 0);
         else for (uint32_t i = 0; i < L; i++) pout[off + i] = 0;
@@ -868,8 +856,9 @@ hipError_t launch_keygen(int mode, const KeyArg& key, const NonceArg& nonce0, ui
 hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const uint8_t* src, uint8_t* dst,
                         uint8_t* ok, hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
-  if (seal) hipLaunchKernelGGL(xs_crypt<true>, dim3((unsigned)nblocks), dim3(256), 0, stream, keys, src, dst, ok);
-  else hipLaunchKernelGGL(xs_crypt<false>, dim3((unsigned)nblocks), dim3(256), 0, stream, keys, src, dst, ok);
+  const unsigned grid = (unsigned)((nblocks + 3) / 4);  // four blocks (waves) per workgroup
+  if (seal) hipLaunchKernelGGL(xs_crypt<true>, dim3(grid), dim3(256), 0, stream, keys, nblocks, src, dst, ok);
+  else hipLaunchKernelGGL(xs_crypt<false>, dim3(grid), dim3(256), 0, stream, keys, nblocks, src, dst, ok);
   return hipGetLastError();
 }
 
