@@ -35,6 +35,7 @@ BLOCK_SIZE = 65552
 # (the 960-byte per-block key schedule is this design's own intermediate, not counted)
 ALG_BYTES_SEAL = 65536 + 65552
 ALG_BYTES_OPEN = 65552 + 65536 + 1
+VALU_CYC, SIMDS, CLOCK_HZ = 4, 256 * 4, 2.4e9
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -89,9 +90,36 @@ def load_traffic():
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get("seal_bytes_per_launch"), d.get("open_bytes_per_launch"), d.get("source")
+        return d
     except Exception:
         return None
+
+
+def sustained_clock():
+    """Shader clock measured under this kernel's own load (profiles/clock_probe.json)."""
+    p = os.path.join(ROOT, "profiles", "clock_probe.json")
+    try:
+        with open(p) as f:
+            return float(json.load(f)["sustained_shader_clock_ghz"]) * 1e9
+    except Exception:
+        return None
+
+
+def issue_bound(valu_insts, ms):
+    """VALU issue bound of a launch: integer VALU wave-instructions x 4 cycles (measured on
+    gfx950: tools/microbench/issuebench.hip) spread over 256 CUs x 4 SIMDs, at the 2.4 GHz peak
+    clock and at the sustained clock measured under this kernel (profiles/clock_probe.json)."""
+    if not valu_insts:
+        return None
+    bound_ms = valu_insts * VALU_CYC / (SIMDS * CLOCK_HZ) * 1e3
+    res = {"valu_wave_insts": valu_insts, "cycles_per_inst": VALU_CYC, "bound_ms_2p4ghz": round(bound_ms, 4),
+           "frac_2p4ghz": round(bound_ms / ms, 4)}
+    clk = sustained_clock()
+    if clk:
+        b2 = valu_insts * VALU_CYC / (SIMDS * clk) * 1e3
+        res.update({"sustained_clock_ghz": round(clk / 1e9, 3), "bound_ms_sustained": round(b2, 4),
+                    "frac_sustained": round(b2 / ms, 4)})
+    return res
 
 
 def main():
@@ -196,10 +224,14 @@ def main():
     if rank == 0:
         ach_seal = ALG_BYTES_SEAL * nb / (seal_avg * 1e-3) / 1e9
         ach_open = ALG_BYTES_OPEN * nb / (open_avg * 1e-3) / 1e9
-        tr = load_traffic()
-        traffic = None
-        if tr and tr[0]:
-            traffic = {"seal": tr[0], "open": tr[1], "source": tr[2]}
+        tr = load_traffic() or {}
+        # PMC figures are per launch of the default workload; scale if nb differs
+        pmc_nb = tr.get("blocks_per_launch", nb)
+        scale = nb / pmc_nb if pmc_nb else 1.0
+
+        def per(key):
+            v = tr.get(key)
+            return round(v * scale) if v else None
         res = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -220,15 +252,18 @@ def main():
                        "parallelism": f"{world} rank(s), blocks sharded, no data-path collective"},
             "seal_GiB_s": round(nb * BLOCK_DATA / 2**30 / (seal_avg * 1e-3), 3),
             "open_GiB_s": round(nb * BLOCK_DATA / 2**30 / (open_avg * 1e-3), 3),
-            "roofline": {"bound": "hbm", "kernel": "xs_crypt<seal>",
+            "roofline": {"bound": "hbm", "kernel": "xs_seal",
                          "achieved": round(ach_seal, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach_seal / HBM_PEAK_GBS, 4),
-                         "traffic": traffic["seal"] if traffic else None,
+                         "traffic": per("seal_bytes_per_launch"),
                          "kernel_ms_avg": round(seal_avg, 4),
                          "alg_bytes_per_launch": ALG_BYTES_SEAL * nb,
-                         "open": {"kernel": "xs_crypt<open>", "achieved": round(ach_open, 1),
+                         "traffic_source": tr.get("source"),
+                         "valu_issue": issue_bound(per("seal_valu_wave_insts_per_launch"), seal_avg),
+                         "open": {"kernel": "xs_open", "achieved": round(ach_open, 1),
                                   "frac": round(ach_open / HBM_PEAK_GBS, 4), "kernel_ms_avg": round(open_avg, 4),
-                                  "traffic": traffic["open"] if traffic else None}},
+                                  "traffic": per("open_bytes_per_launch"),
+                                  "valu_issue": issue_bound(per("open_valu_wave_insts_per_launch"), open_avg)}},
             "counters": {"blocks": int(counters[0].item()), "bytes": total_bytes,
                          "tag_failures": int(counters[2].item())},
             "cpu_baseline": None,

@@ -2,7 +2,7 @@
 //
 // Replaces the per-block secretbox.Seal / secretbox.Open calls of backend/crypt
 // (cipher.go:737, :880) with batched launches: xs_keygen (per-block key schedule) then
-// xs_crypt (one 64 KiB block per workgroup).  The engine keeps per-slot device buffers and
+// xs_seal/xs_open (one 64 KiB block per wave64).  The engine keeps per-slot device buffers and
 // streams so host->device copies, kernels and device->host copies of consecutive batches
 // overlap (the host-path number in DESIGN.md).
 #include <hip/hip_runtime.h>

@@ -40,5 +40,8 @@ hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const
 hipError_t launch_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, hipStream_t stream);
 
 void set_error(const char* fmt, ...);
+#ifdef XS_CLOCK_PROBE
+void probe_read(unsigned long long* host, size_t n);
+#endif
 
 }  // namespace xs

@@ -9,7 +9,7 @@
 //              block 0 (Poly1305 key r||s), keystream block 1024 words 0..7 (the last
 //              two 16-byte chunks of a full block) and the Poly1305 power tables the
 //              main kernel needs (r, r^253, r^0..31, r^(32a)).  ~2% of the work.
-//   xs_crypt   one 64 KiB block per wave64 (four per 256-lane workgroup).  Lane l owns the
+//   xs_seal / xs_open   one 64 KiB block per wave64 (four per 256-lane workgroup).  Lane l owns the
 //              Salsa20 keystream blocks K = l + 64*s (s = 0..15), i.e. message chunks
 //              4K-2 .. 4K+1 (16 bytes each, offset by the 32-byte Poly1305 key).  A lane
 //              keeps the whole 16-word Salsa20 state in VGPRs; key/nonce words are
@@ -29,9 +29,13 @@
 
 #include "xs_internal.h"
 
-// XS_WAVES_PER_EU: occupancy hint for diagnostic builds (tools/ablate.cpp); product = 1.
-#ifndef XS_WAVES_PER_EU
-#define XS_WAVES_PER_EU 1
+// XS_SEAL_WPE / XS_OPEN_WPE: minimum waves per SIMD the register allocator must allow
+// (amdgpu_waves_per_eu) for the seal / open kernels.
+#ifndef XS_SEAL_WPE
+#define XS_SEAL_WPE 1
+#endif
+#ifndef XS_OPEN_WPE
+#define XS_OPEN_WPE 1
 #endif
 
 
@@ -764,12 +768,9 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
 }
 
 template <bool SEAL>
-__global__ void __launch_bounds__(256, XS_WAVES_PER_EU) xs_crypt(const BlockKey* __restrict__ keys,
-                                                                 uint64_t nblocks,
-                                                                 const uint8_t* __restrict__ src,
-                                                                 uint8_t* __restrict__ dst,
-                                                                 uint8_t* __restrict__ ok) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
+__device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, uint64_t nblocks,
+                                           const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                           uint8_t* __restrict__ ok, uint32_t* lds) {
   const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63u;
   // wave-uniform block index
   const uint64_t blk = (uint64_t)blockIdx.x * 4u + (uint64_t)__builtin_amdgcn_readfirstlane(wave);
@@ -827,6 +828,42 @@ __global__ void __launch_bounds__(256, XS_WAVES_PER_EU) xs_crypt(const BlockKey*
   }
 }
 
+#ifdef XS_CLOCK_PROBE
+// Diagnostic build only (tools/ablate.cpp): wave 0 of every workgroup records the shader
+// clock (s_memtime) and the 100 MHz constant clock (s_memrealtime) at entry and exit, giving
+// the sustained shader clock under this kernel's own load.
+__device__ unsigned long long xs_probe[4 * 65536];
+#define XS_PROBE_BEGIN                                                   \
+  const unsigned long long pt0 = __builtin_amdgcn_s_memtime();           \
+  const unsigned long long pr0 = __builtin_amdgcn_s_memrealtime();
+#define XS_PROBE_END                                                     \
+  if (threadIdx.x == 0 && blockIdx.x < 65536) {                          \
+    xs_probe[4 * blockIdx.x + 0] = pt0;                                  \
+    xs_probe[4 * blockIdx.x + 1] = pr0;                                  \
+    xs_probe[4 * blockIdx.x + 2] = __builtin_amdgcn_s_memtime();         \
+    xs_probe[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();     \
+  }
+#else
+#define XS_PROBE_BEGIN
+#define XS_PROBE_END
+#endif
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XS_SEAL_WPE)))
+xs_seal(const BlockKey* __restrict__ keys, uint64_t nblocks, const uint8_t* __restrict__ src,
+        uint8_t* __restrict__ dst) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
+  XS_PROBE_BEGIN
+  crypt_wave<true>(keys, nblocks, src, dst, nullptr, lds);
+  XS_PROBE_END
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XS_OPEN_WPE)))
+xs_open(const BlockKey* __restrict__ keys, uint64_t nblocks, const uint8_t* __restrict__ src,
+        uint8_t* __restrict__ dst, uint8_t* __restrict__ ok) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
+  crypt_wave<false>(keys, nblocks, src, dst, ok, lds);
+}
+
 // SplitMix64 fill (synthetic benchmark objects generated in HBM): word k = mix(seed + (k+1)*golden)
 __global__ void xs_fill_splitmix(uint64_t* __restrict__ dst, uint64_t nwords, uint64_t seed) {
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nwords;
@@ -853,12 +890,18 @@ hipError_t launch_keygen(int mode, const KeyArg& key, const NonceArg& nonce0, ui
   return hipGetLastError();
 }
 
+#ifdef XS_CLOCK_PROBE
+void probe_read(unsigned long long* host, size_t n) {
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(xs_probe), n * sizeof(unsigned long long));
+}
+#endif
+
 hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const uint8_t* src, uint8_t* dst,
                         uint8_t* ok, hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
   const unsigned grid = (unsigned)((nblocks + 3) / 4);  // four blocks (waves) per workgroup
-  if (seal) hipLaunchKernelGGL(xs_crypt<true>, dim3(grid), dim3(256), 0, stream, keys, nblocks, src, dst, ok);
-  else hipLaunchKernelGGL(xs_crypt<false>, dim3(grid), dim3(256), 0, stream, keys, nblocks, src, dst, ok);
+  if (seal) hipLaunchKernelGGL(xs_seal, dim3(grid), dim3(256), 0, stream, keys, nblocks, src, dst);
+  else hipLaunchKernelGGL(xs_open, dim3(grid), dim3(256), 0, stream, keys, nblocks, src, dst, ok);
   return hipGetLastError();
 }
 

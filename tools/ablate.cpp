@@ -4,13 +4,14 @@
 #include <cstdio>
 #include <cstdint>
 #include <vector>
+#include <algorithm>
 #include "../rclone_amd/csrc/xs_internal.h"
 
 int main(int argc, char** argv) {
   const uint64_t nb = 100000;
   uint8_t *plain, *body; xs::BlockKey* ws;
   (void)hipMalloc(&plain, nb * 65536); (void)hipMalloc(&body, nb * 65552); (void)hipMalloc(&ws, nb * sizeof(xs::BlockKey));
-  (void)hipMemset(plain, 7, nb * 65536);
+  (void)xs::launch_fill(reinterpret_cast<uint64_t*>(plain), nb * 65536 / 8, 12345, 0);  // random, like bench.py
   xs::KeyArg k{}; xs::NonceArg n{};
   for (int i = 0; i < 8; i++) k.k[i] = 0x01020304u * (i + 1);
   uint8_t* okb; xs::BlockKey* ws2; uint8_t* out;
@@ -25,15 +26,32 @@ int main(int argc, char** argv) {
     };
     for (int r = 0; r < 2; r++) go();
     (void)hipDeviceSynchronize();
-    float best = 1e9, tot = 0;
-    for (int r = 0; r < 5; r++) {
+    std::vector<float> t;
+    for (int r = 0; r < 25; r++) {
       (void)hipEventRecord(a);
       go();
       (void)hipEventRecord(b); (void)hipEventSynchronize(b);
-      float ms; (void)hipEventElapsedTime(&ms, a, b); tot += ms; if (ms < best) best = ms;
+      float ms; (void)hipEventElapsedTime(&ms, a, b); t.push_back(ms);
     }
-    printf("%s %s: best %.3f ms avg %.3f ms  (%.1f GiB/s)  err=%s\n", argc > 1 ? argv[1] : "", dir ? "open" : "seal",
-           best, tot / 5, nb * 65536.0 / 1073741824.0 / (best * 1e-3), hipGetErrorString(hipGetLastError()));
+    std::sort(t.begin(), t.end());
+    printf("%s %s: min %.3f ms median %.3f ms  (%.1f GiB/s at median)  err=%s\n", argc > 1 ? argv[1] : "",
+           dir ? "open" : "seal", t[0], t[12], nb * 65536.0 / 1073741824.0 / (t[12] * 1e-3),
+           hipGetErrorString(hipGetLastError()));
   }
+#ifdef XS_CLOCK_PROBE
+  // last launch was open; re-run one seal and read the per-workgroup clocks
+  (void)xs::launch_crypt(true, ws, nb, plain, body, nullptr, 0);
+  (void)hipDeviceSynchronize();
+  const size_t nwg = (nb + 3) / 4;
+  std::vector<unsigned long long> pr(4 * nwg);
+  xs::probe_read(pr.data(), pr.size());
+  double sum = 0, mn = 1e30, mx = 0;
+  for (size_t i = 0; i < nwg; i++) {
+    const double f = (double)(pr[4 * i + 2] - pr[4 * i]) / (double)(pr[4 * i + 3] - pr[4 * i + 1]) * 100e6;
+    sum += f; mn = f < mn ? f : mn; mx = f > mx ? f : mx;
+  }
+  printf("shader clock under seal load: mean %.3f GHz  min %.3f  max %.3f  (%zu workgroups)\n", sum / nwg / 1e9,
+         mn / 1e9, mx / 1e9, nwg);
+#endif
   return 0;
 }

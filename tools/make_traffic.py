@@ -4,7 +4,8 @@ xs_crypt launch: profiles/pmc_traffic.json (read by bench.py as roofline.traffic
 
 Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE counts exactly half the
 bytes of a wide (16 B/lane) streaming read -- global_load and LDS-DMA alike -- so reads =
-2 x FETCH_SIZE; WRITE_SIZE is exact for 16 B/lane stores.  Both are in KiB."""
+2 x FETCH_SIZE; WRITE_SIZE is exact for 16 B/lane stores.  Both are in KiB.
+Also records SQ_INSTS_VALU (wave-instructions) per launch for the VALU issue bound."""
 import json
 import os
 import sys
@@ -16,15 +17,20 @@ from pmc_summary import load  # noqa: E402
 def main():
     d, out = sys.argv[1], sys.argv[2]
     acc = load(d)
-    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE ({d}), reads x2 (gfx950 FETCH_SIZE halving)"}
+    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE ({d}), reads x2 (gfx950 FETCH_SIZE halving)",
+           "blocks_per_launch": int(sys.argv[3]) if len(sys.argv) > 3 else 100_000}
     for k, cs in acc.items():
-        for name, key in (("xs_crypt<true>", "seal"), ("xs_crypt<false>", "open")):
+        for name, key in (("xs_seal", "seal"), ("xs_open", "open")):
             if name in k and "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
                 fetch = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"]) * 1024 * 2
                 write = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) * 1024
                 res[f"{key}_read_bytes_per_launch"] = round(fetch)
                 res[f"{key}_write_bytes_per_launch"] = round(write)
                 res[f"{key}_bytes_per_launch"] = round(fetch + write)
+            if name in k and "SQ_INSTS_VALU" in cs:
+                res[f"{key}_valu_wave_insts_per_launch"] = round(sum(cs["SQ_INSTS_VALU"]) / len(cs["SQ_INSTS_VALU"]))
+                if "SQ_WAVES" in cs:
+                    res[f"{key}_waves_per_launch"] = round(sum(cs["SQ_WAVES"]) / len(cs["SQ_WAVES"]))
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))

@@ -20,7 +20,7 @@ def load(d):
 
 def main():
     d = sys.argv[1]
-    subs = sys.argv[2:] or ["xs_crypt<true>", "xs_crypt<false>", "xs_keygen"]
+    subs = sys.argv[2:] or ["xs_seal", "xs_open", "xs_keygen"]
     acc = load(d)
     out = {}
     for k, cs in acc.items():
