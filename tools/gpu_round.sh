@@ -16,4 +16,5 @@ cat gpurun_out/$TAG.hostpath.json
 export TMPDIR=/tmp
 cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/$TAG.prof -- python3 $R/bench.py --no-cpu > $R/gpurun_out/$TAG.prof.log 2>&1 || { echo PROF_FAILED; tail $R/gpurun_out/$TAG.prof.log; exit 1; }
 tail -1 $R/gpurun_out/$TAG.prof.log
+python3 $R/tools/prof_agree.py $R/gpurun_out/$TAG.prof $R/gpurun_out/$TAG.prof.log $R/gpurun_out/$TAG.timing_agreement.json
 echo ROUND_DONE
