@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--blocks", type=int, default=100_000, help="64 KiB blocks per GPU")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--object-blocks", type=int, default=0,
+                    help="configs[3] mode: one logical object of this many blocks (2^24 = 1 TiB) split "
+                         "round-robin over the ranks, processed in --blocks rounds with on-device "
+                         "generation inside each step (0 = the default resident-set bench)")
     return ap.parse_args()
 
 
@@ -122,6 +126,65 @@ def issue_bound(valu_insts, ms):
     return res
 
 
+def run_objectset(args, world, rank, dev, dist):
+    """BASELINE configs[3]: the rank's round-robin share of an --object-blocks object, in
+    --blocks rounds; one step = every round (generate in HBM, seal, open, verify, digest)."""
+    import torch
+
+    from rclone_amd import shard
+    from rclone_amd.objectset import RankRunner, digest_to_u64
+    key = bytes(range(32))
+    nonce0 = bytes([0xF0]) + bytes([0xFF] * 7) + bytes(16)
+    r = RankRunner(key, nonce0, args.object_blocks, world, rank, args.blocks, 0x5EED, dev)
+    for _ in range(args.warmup):
+        r.run_round(0)
+    torch.cuda.synchronize(dev)
+    r.counters.zero_()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r.run_all(record=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    counters = r.counters.clone()
+    tmax = torch.tensor([el], dtype=torch.float64, device=dev)
+    shard.reduce_counters(counters, dist if world > 1 else None)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    el = float(tmax.item())
+    blocks, nbytes, fails, mism, d0, d1 = digest_to_u64(counters)
+    if fails or mism or blocks != args.steps * args.object_blocks:
+        raise SystemExit(f"bench: object set failed (blocks {blocks}, tag failures {fails}, mismatches {mism})")
+    seal_ms = [a.elapsed_time(b) for s, a, b in r.kernel_events if s]
+    open_ms = [a.elapsed_time(b) for s, a, b in r.kernel_events if not s]
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(2 * nbytes / 2**30 / el, 3),
+            "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (SplitMix64 keyed by global block id, generated in HBM inside each step)",
+            "config": {"workload": f"one {args.object_blocks}-block object ({args.object_blocks * BLOCK_DATA / 2**40:.3f} "
+                                   f"TiB) round-robin over {world} rank(s), {args.blocks}-block rounds, seal then "
+                                   f"open+verify (BASELINE configs[3])",
+                       "object_blocks": args.object_blocks, "round_blocks": args.blocks,
+                       "parallelism": f"{world} rank(s), blocks sharded, counters all-reduced"},
+            "seal_kernel_GiB_s": round(r.n * BLOCK_DATA * args.steps / 2**30 / (sum(seal_ms) * 1e-3), 3),
+            "open_kernel_GiB_s": round(r.n * BLOCK_DATA * args.steps / 2**30 / (sum(open_ms) * 1e-3), 3),
+            "counters": {"blocks": blocks, "bytes": nbytes, "tag_failures": fails, "roundtrip_mismatch_rounds": mism,
+                         "tag_digest": f"{d1:016x}{d0:016x}"},
+            "roofline": None, "cpu_baseline": None,
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     import torch
@@ -135,6 +198,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+
+    if args.object_blocks:
+        return run_objectset(args, world, rank, dev, dist)
 
     import numpy as np
 
@@ -151,7 +217,7 @@ def main():
     d_seal = torch.from_numpy(shard.seal_descriptors(nonce0, gidx).view(np.uint8).copy()).to(dev)
     d_open = torch.from_numpy(shard.seal_descriptors(nonce0, gidx, open_mode=True).view(np.uint8).copy()).to(dev)
     plain = torch.empty(plain_len, dtype=torch.uint8, device=dev)
-    device.fill_random(plain, 0x5EED + rank)
+    device.fill_blocks(plain, rank, world, 0x5EED)  # global block g = rank + world*i, keyed by g
     body = torch.empty(body_len, dtype=torch.uint8, device=dev)
     out = torch.empty(plain_len, dtype=torch.uint8, device=dev)
     ok = torch.empty(nb, dtype=torch.uint8, device=dev)
@@ -208,8 +274,10 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     # counters and max time over ranks (RCCL, small tensors only)
-    counters = torch.tensor([args.steps * 2 * nb, args.steps * 2 * plain_len, int(nb - int(ok.sum()))],
+    from rclone_amd.objectset import tag_digest
+    counters = torch.tensor([args.steps * 2 * nb, args.steps * 2 * plain_len, int(nb - int(ok.sum())), 0, 0],
                             dtype=torch.int64, device=dev)
+    counters[3:5] = tag_digest(body, nb)  # order-independent: the same for any world size
     tmax = torch.tensor([el], dtype=torch.float64, device=dev)
     shard.reduce_counters(counters, dist if world > 1 else None)
     if world > 1:
@@ -265,7 +333,9 @@ def main():
                                   "traffic": per("open_bytes_per_launch"),
                                   "valu_issue": issue_bound(per("open_valu_wave_insts_per_launch"), open_avg)}},
             "counters": {"blocks": int(counters[0].item()), "bytes": total_bytes,
-                         "tag_failures": int(counters[2].item())},
+                         "tag_failures": int(counters[2].item()),
+                         "tag_digest": "%016x%016x" % (int(counters[4].item()) & (2**64 - 1),
+                                                       int(counters[3].item()) & (2**64 - 1))},
             "cpu_baseline": None,
         }
         if not args.no_cpu:

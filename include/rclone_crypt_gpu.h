@@ -103,6 +103,10 @@ int xs_keygen_batch_dev(int seal, const uint8_t key[32], const xs_block_desc *d_
                         void *d_workspace, void *stream);
 /* Fill d with the SplitMix64 stream (word k = mix(seed + (k+1)*0x9E3779B97F4A7C15)). */
 int xs_fill_random_dev(void *d, uint64_t nbytes, uint64_t seed, void *stream);
+/* Fill nblocks 64 KiB blocks: local block b = global block first_block + b*block_stride of the
+ * same stream (a rank's round-robin share of a synthetic object set, BASELINE configs[3]). */
+int xs_fill_blocks_dev(void *d, uint64_t nblocks, uint64_t first_block, uint64_t block_stride, uint64_t seed,
+                       void *stream);
 
 /* Host-memory engine: pinned staging, per-slot streams, H2D/kernel/D2H overlapped. */
 typedef struct xs_engine xs_engine;

@@ -46,6 +46,10 @@ def _load():
     lib.orc_seal_blocks.restype = ctypes.c_int
     lib.orc_open_blocks.argtypes = [vp, vp, vp, ctypes.c_int64, c_p, c_p]
     lib.orc_open_blocks.restype = ctypes.c_int
+    lib.orc_seal_desc.argtypes = [vp, vp, vp, ctypes.c_int64, c_p]
+    lib.orc_seal_desc.restype = ctypes.c_int
+    lib.orc_open_desc.argtypes = [vp, vp, vp, vp, ctypes.c_int64, c_p]
+    lib.orc_open_desc.restype = ctypes.c_int
     return lib
 
 
@@ -116,3 +120,16 @@ def decrypt_file(ct: bytes, key: bytes, pass_bad_blocks=False):
     if rc < 0:
         return None, rc, bad.value
     return out.raw[:rc], 0, -1
+
+
+def seal_desc(dst, src, desc, key: bytes) -> int:
+    """Seal every descriptor (numpy structured array, xs_block_desc layout) from the numpy
+    u8 array src into dst (both host arrays).  Returns the OpenMP thread count."""
+    assert desc.dtype.itemsize == 48
+    return lib().orc_seal_desc(dst.ctypes.data, src.ctypes.data, desc.ctypes.data, len(desc), bytes(key))
+
+
+def open_desc(dst, ok, src, desc, key: bytes) -> int:
+    assert desc.dtype.itemsize == 48
+    return lib().orc_open_desc(dst.ctypes.data, ok.ctypes.data, src.ctypes.data, desc.ctypes.data, len(desc),
+                               bytes(key))

@@ -354,3 +354,45 @@ int orc_open_blocks(uint8_t *out, uint8_t *ok, const uint8_t *in, int64_t nblock
   }
   return threads;
 }
+
+/* Descriptor-mode batches (test checker for xs_seal_batch_dev / xs_open_batch_dev): each
+ * descriptor is one secretbox of `len` bytes with its own 24-byte nonce, i.e. one
+ * encrypter.Read block (cipher.go:737) / decrypter.fillBuffer block (cipher.go:880).  Same
+ * 48-byte layout as xs_block_desc.  OpenMP over descriptors; returns the thread count. */
+typedef struct orc_desc {
+  uint64_t src_off;
+  uint64_t dst_off;
+  uint32_t len;
+  uint32_t reserved;
+  uint8_t nonce[24];
+} orc_desc;
+
+int orc_seal_desc(uint8_t *dst, const uint8_t *src, const orc_desc *d, int64_t n, const uint8_t key[32]) {
+  int threads = 1;
+#pragma omp parallel
+  {
+#ifdef _OPENMP
+#pragma omp single
+    threads = omp_get_num_threads();
+#endif
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t i = 0; i < n; i++)
+      orc_secretbox_seal(dst + d[i].dst_off, src + d[i].src_off, d[i].len, d[i].nonce, key);
+  }
+  return threads;
+}
+
+int orc_open_desc(uint8_t *dst, uint8_t *ok, const uint8_t *src, const orc_desc *d, int64_t n, const uint8_t key[32]) {
+  int threads = 1;
+#pragma omp parallel
+  {
+#ifdef _OPENMP
+#pragma omp single
+    threads = omp_get_num_threads();
+#endif
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t i = 0; i < n; i++)
+      ok[i] = orc_secretbox_open(dst + d[i].dst_off, src + d[i].src_off, (size_t)d[i].len + ORC_BLOCK_HDR, d[i].nonce, key) == 0;
+  }
+  return threads;
+}

@@ -212,7 +212,18 @@ int xs_fill_random_dev(void* d, uint64_t nbytes, uint64_t seed, void* stream) {
     set_error("xs_fill_random_dev: need a 16-byte aligned buffer and a multiple of 8 bytes");
     return XS_ERR_INVALID;
   }
-  hipError_t e = launch_fill((uint64_t*)d, nbytes / 8, seed, (hipStream_t)stream);
+  hipError_t e = launch_fill((uint64_t*)d, nbytes / 8, seed, 0, 1, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "fill launch");
+  return XS_OK;
+}
+
+int xs_fill_blocks_dev(void* d, uint64_t nblocks, uint64_t first_block, uint64_t block_stride, uint64_t seed,
+                       void* stream) {
+  if (!d || !aligned16(d) || block_stride == 0) {
+    set_error("xs_fill_blocks_dev: need a 16-byte aligned buffer and block_stride >= 1");
+    return XS_ERR_INVALID;
+  }
+  hipError_t e = launch_fill((uint64_t*)d, nblocks * 8192u, seed, first_block, block_stride, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "fill launch");
   return XS_OK;
 }

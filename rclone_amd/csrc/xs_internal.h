@@ -37,7 +37,8 @@ hipError_t launch_keygen(int mode, const KeyArg& key, const NonceArg& nonce0, ui
                          hipStream_t stream);
 hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const uint8_t* src, uint8_t* dst,
                         uint8_t* ok, hipStream_t stream);
-hipError_t launch_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, hipStream_t stream);
+hipError_t launch_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t first_block, uint64_t stride,
+                       hipStream_t stream);
 
 void set_error(const char* fmt, ...);
 #ifdef XS_CLOCK_PROBE

@@ -864,11 +864,16 @@ xs_open(const BlockKey* __restrict__ keys, uint64_t nblocks, const uint8_t* __re
   crypt_wave<false>(keys, nblocks, src, dst, ok, lds);
 }
 
-// SplitMix64 fill (synthetic benchmark objects generated in HBM): word k = mix(seed + (k+1)*golden)
-__global__ void xs_fill_splitmix(uint64_t* __restrict__ dst, uint64_t nwords, uint64_t seed) {
+// SplitMix64 fill (synthetic benchmark objects generated in HBM).  Global word g of the stream
+// is mix(seed + (g+1)*golden); local 64 KiB block b of the buffer holds global block
+// first_block + b*stride (8192 words per block), so a rank's round-robin share of an object
+// set gets the same bytes whatever the world size.  stride 1, first_block 0 = plain stream.
+__global__ void xs_fill_splitmix(uint64_t* __restrict__ dst, uint64_t nwords, uint64_t seed, uint64_t first_block,
+                                 uint64_t stride) {
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nwords;
        k += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t z = seed + (k + 1) * 0x9E3779B97F4A7C15ull;
+    const uint64_t g = (first_block + (k >> 13) * stride) * 8192u + (k & 8191u);
+    uint64_t z = seed + (g + 1) * 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     dst[k] = z ^ (z >> 31);
@@ -905,11 +910,13 @@ hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const
   return hipGetLastError();
 }
 
-hipError_t launch_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, hipStream_t stream) {
+hipError_t launch_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t first_block, uint64_t stride,
+                       hipStream_t stream) {
   if (nwords == 0) return hipSuccess;
   uint64_t grid = (nwords + 255) / 256;
   if (grid > 8192) grid = 8192;
-  hipLaunchKernelGGL(xs_fill_splitmix, dim3((unsigned)grid), dim3(256), 0, stream, dst, nwords, seed);
+  hipLaunchKernelGGL(xs_fill_splitmix, dim3((unsigned)grid), dim3(256), 0, stream, dst, nwords, seed, first_block,
+                     stride);
   return hipGetLastError();
 }
 

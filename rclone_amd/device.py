@@ -95,3 +95,61 @@ def fill_random(t: torch.Tensor, seed: int):
     rc = _lib.lib().xs_fill_random_dev(t.data_ptr(), t.numel() * t.element_size(), seed, _stream(t))
     _lib.check(rc, "xs_fill_random_dev")
     return t
+
+
+def fill_blocks(t: torch.Tensor, first_block: int, block_stride: int, seed: int):
+    """Fill t (whole 64 KiB blocks) with global blocks first_block + b*block_stride of the
+    SplitMix64 stream that fill_random(seed) lays out contiguously."""
+    _require_gpu(t)
+    nbytes = t.numel() * t.element_size()
+    if nbytes % BLOCK_DATA:
+        raise ValueError("fill_blocks needs whole 64 KiB blocks")
+    rc = _lib.lib().xs_fill_blocks_dev(t.data_ptr(), nbytes // BLOCK_DATA, first_block, block_stride, seed, _stream(t))
+    _lib.check(rc, "xs_fill_blocks_dev")
+    return t
+
+
+def _desc_tensor(desc, device):
+    """xs_block_desc array (numpy structured, 48 B/entry, or a uint8 device tensor) on device."""
+    if isinstance(desc, torch.Tensor):
+        _require_gpu(desc)
+        assert desc.numel() % 48 == 0
+        return desc
+    import numpy as np
+    assert desc.dtype.itemsize == 48
+    raw = np.frombuffer(desc.tobytes(), dtype=np.uint8)
+    return torch.from_numpy(raw.copy()).to(device)
+
+
+def seal_batch(key: bytes, desc, src: torch.Tensor, dst: torch.Tensor, ws: torch.Tensor = None):
+    """Seal one secretbox per descriptor (xs_seal_batch_dev): src[src_off:+len] ->
+    dst[dst_off:+16+len] with the descriptor's own nonce.  Invalid descriptors are skipped."""
+    _require_gpu(src, dst)
+    d = _desc_tensor(desc, src.device)
+    nb = d.numel() // 48
+    if ws is None:
+        ws = workspace(nb, src.device)
+    _require_gpu(ws)
+    rc = _lib.lib().xs_seal_batch_dev(bytes(key), d.data_ptr(), nb, src.data_ptr(), src.numel(), dst.data_ptr(),
+                                      dst.numel(), ws.data_ptr(), _stream(src))
+    _lib.check(rc, "xs_seal_batch_dev")
+    return dst
+
+
+def open_batch(key: bytes, desc, src: torch.Tensor, dst: torch.Tensor, ok: torch.Tensor = None,
+               ws: torch.Tensor = None) -> torch.Tensor:
+    """Open one secretbox per descriptor (xs_open_batch_dev): src[src_off:+16+len] (tag||ct) ->
+    dst[dst_off:+len]; returns ok (uint8 per descriptor; failed blocks are zero-filled,
+    invalid descriptors write nothing and report 0)."""
+    _require_gpu(src, dst)
+    d = _desc_tensor(desc, src.device)
+    nb = d.numel() // 48
+    if ok is None:
+        ok = torch.empty(max(nb, 1), dtype=torch.uint8, device=src.device)
+    if ws is None:
+        ws = workspace(nb, src.device)
+    _require_gpu(ok, ws)
+    rc = _lib.lib().xs_open_batch_dev(bytes(key), d.data_ptr(), nb, src.data_ptr(), src.numel(), dst.data_ptr(),
+                                      dst.numel(), ok.data_ptr(), ws.data_ptr(), _stream(src))
+    _lib.check(rc, "xs_open_batch_dev")
+    return ok[:nb]

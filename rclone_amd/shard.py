@@ -23,11 +23,21 @@ def owned_blocks(total_blocks: int, world: int, rank: int) -> np.ndarray:
 
 
 def nonce_plus(nonce0: bytes, idx: np.ndarray) -> np.ndarray:
-    """nonce0 + idx as 24-byte little-endian numbers (nonce.add, cipher.go:665) -> (n, 24) u8."""
-    base = int.from_bytes(bytes(nonce0), "little")
+    """nonce0 + idx as 24-byte little-endian numbers (nonce.add, cipher.go:665) -> (n, 24) u8.
+    Vectorised: 64-bit add of the low word, carries into bytes 8.. handled per carrying row."""
+    idx = np.asarray(idx, dtype=np.uint64)
+    n0 = bytes(nonce0)
+    lo0 = np.uint64(int.from_bytes(n0[:8], "little"))
     out = np.empty((len(idx), 24), dtype=np.uint8)
-    for j, i in enumerate(idx.tolist()):
-        out[j] = np.frombuffer(((base + int(i)) % (1 << 192)).to_bytes(24, "little"), dtype=np.uint8)
+    with np.errstate(over="ignore"):
+        lo = idx + lo0
+    out[:, :8] = lo.astype("<u8").view(np.uint8).reshape(-1, 8)
+    out[:, 8:] = np.frombuffer(n0[8:], dtype=np.uint8)
+    carry = np.flatnonzero(lo < lo0)
+    if len(carry):
+        hi = int.from_bytes(n0[8:], "little")
+        up = np.frombuffer(((hi + 1) % (1 << 128)).to_bytes(16, "little"), dtype=np.uint8)
+        out[carry, 8:] = up
     return out
 
 

@@ -25,10 +25,10 @@ def pattern_bytes(n: int, offset: int = 0) -> bytes:
     return (i % 251).astype(np.uint8).tobytes()
 
 
-def splitmix64_words(seed: int, nwords: int) -> np.ndarray:
-    """word k = mix(seed + (k + 1) * golden), the standard SplitMix64 sequence."""
+def splitmix64_words(seed: int, nwords: int, first: int = 0) -> np.ndarray:
+    """word k = mix(seed + (k + 1) * golden), the standard SplitMix64 sequence (k from first)."""
     with np.errstate(over="ignore"):
-        z = np.uint64(seed) + (np.arange(1, nwords + 1, dtype=np.uint64) * _GOLDEN)
+        z = np.uint64(seed) + (np.arange(first + 1, first + nwords + 1, dtype=np.uint64) * _GOLDEN)
         z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))
@@ -38,3 +38,8 @@ def splitmix64_words(seed: int, nwords: int) -> np.ndarray:
 def splitmix64_bytes(seed: int, n: int) -> bytes:
     words = splitmix64_words(seed, (n + 7) // 8)
     return words.astype("<u8").tobytes()[:n]
+
+
+def splitmix64_block(seed: int, g: int) -> bytes:
+    """Global 64 KiB block g of the stream (what xs_fill_blocks_dev writes for block g)."""
+    return splitmix64_words(seed, 8192, first=g * 8192).astype("<u8").tobytes()

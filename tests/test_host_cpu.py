@@ -76,3 +76,24 @@ def test_error_strings():
     assert lib.rc_error_string(-106) == b"Seek beyond end of file"
     assert str(crypt.ErrorEncryptedBadMagic(crypt.ErrorEncryptedBadMagic.message)) == \
         "not an encrypted file - bad magic string"
+
+
+def test_nonce_plus_matches_nonce_add():
+    # shard.nonce_plus (vectorised nonce0 + i for descriptor tables) == nonce.add (cipher.go:665)
+    import numpy as np
+
+    from oracle import pyoracle as orc
+    from rclone_amd.shard import nonce_plus
+    idx = np.array([0, 1, 2, 255, 256, 65535, 2**32, 2**63, 2**64 - 1], dtype=np.uint64)
+    for n0 in (bytes(24), b"\xff" * 24, b"\xfe" + b"\xff" * 7 + bytes(range(16)), bytes(range(24)),
+               b"\xff" * 23 + b"\x00"):
+        got = nonce_plus(n0, idx)
+        for j, i in enumerate(idx.tolist()):
+            assert got[j].tobytes() == orc.nonce_add(n0, i), (n0.hex(), i)
+
+
+def test_splitmix_block_stream():
+    from rclone_amd.testdata import splitmix64_block, splitmix64_bytes
+    whole = splitmix64_bytes(7, 5 * 65536)
+    for g in range(5):
+        assert splitmix64_block(7, g) == whole[g * 65536:(g + 1) * 65536]
