@@ -57,6 +57,17 @@ typedef struct xs_block_desc {
   uint8_t nonce[24];
 } xs_block_desc;
 
+/* One MD5 stream for xs_md5_batch_dev: prefix[0:prefix_len] (prefix_len 0, 16 or 32 -- the
+ * 32-byte crypt header "RCLONE\0\0" || nonce, cipher.go:34-37) followed by len bytes at byte
+ * offset off (16-byte aligned) of the source buffer. */
+typedef struct xs_md5_desc {
+  uint64_t off;
+  uint64_t len;
+  uint8_t prefix[32];  /* 16-byte aligned within the (16-byte aligned) descriptor array */
+  uint32_t prefix_len;
+  uint32_t reserved[3];
+} xs_md5_desc;  /* 64 bytes */
+
 const char *xs_version(void);
 /* Last error message of the calling thread ("" if none). */
 const char *xs_last_error(void);
@@ -108,6 +119,13 @@ int xs_fill_random_dev(void *d, uint64_t nbytes, uint64_t seed, void *stream);
 int xs_fill_blocks_dev(void *d, uint64_t nblocks, uint64_t first_block, uint64_t block_stride, uint64_t seed,
                        void *stream);
 
+/* MD5 of n streams in HBM, one lane per stream (crypt.go:516-533 put's ciphertext hash,
+ * :784-806 computeHashWithNonce): d_digest[16*i] = MD5(prefix_i || src[off_i : off_i+len_i]).
+ * An invalid descriptor (bounds, alignment, prefix_len) gets d_ok[i] = 0 (d_ok may be NULL)
+ * and an unspecified digest. */
+int xs_md5_batch_dev(const xs_md5_desc *d_desc, uint64_t n, const void *d_src, uint64_t src_len,
+                     uint8_t *d_digest, uint8_t *d_ok, void *stream);
+
 /* Host-memory engine: pinned staging, per-slot streams, H2D/kernel/D2H overlapped. */
 typedef struct xs_engine xs_engine;
 xs_engine *xs_engine_create(int device, uint32_t batch_blocks, int nslots);
@@ -116,6 +134,14 @@ int xs_engine_seal(xs_engine *e, const uint8_t key[32], const uint8_t nonce0[24]
                    const void *plain, uint64_t plain_len, void *body);
 int xs_engine_open(xs_engine *e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
                    const void *body, uint64_t body_len, void *plain, uint8_t *ok);
+/* Seal many host objects and MD5 their crypt files on the GPU -- the hash Fs.put tees off the
+ * ciphertext (crypt.go:516-533) and cryptcheck's computeHashWithNonce (crypt.go:784-806),
+ * batched across objects: object i = plain[offs[i] : offs[i]+lens[i]] (offs 16-byte aligned),
+ * block j sealed with nonces[24i..] + j; md5[16i..] = MD5("RCLONE\0\0" || nonce_i || wire
+ * blocks).  Only the digests come back over PCIe.  MD5 runs one GPU lane per object, so this
+ * pays off for many objects per call (hundreds+), not for one large stream. */
+int xs_engine_seal_md5(xs_engine *e, const uint8_t key[32], uint64_t nobj, const uint8_t *nonces,
+                       const uint64_t *offs, const uint64_t *lens, const void *plain, uint8_t *md5);
 /* Pinned (page-locked) host memory. */
 void *xs_host_alloc(size_t bytes);
 void xs_host_free(void *p);
@@ -200,6 +226,16 @@ void rc_decrypter_nonce(const rc_decrypter *d, uint8_t out[24]);
 /* error wrapped by RC_ERR_REOPEN / RC_ERR_SHORT_NONCE (the %w operand) */
 int32_t rc_decrypter_wrapped_error(const rc_decrypter *d);
 void rc_decrypter_free(rc_decrypter *d);
+
+/* Fs.computeHashWithNonce (crypt.go:784-806) for MD5, batched over n source objects -- the
+ * cryptcheck / bisync check path (cmd/cryptcheck/cryptcheck.go:67-117): reads srcs[i] to EOF
+ * in 64 KiB ReadFills (as newEncrypter would), closes it if it has a close function
+ * (fs.CheckClose), seals it with nonces[24i..] and MD5s the crypt file, all on the GPU
+ * (xs_engine_seal_md5).  errs[i] = RC_NIL with md5[16i..] set, or the reader's / closer's
+ * error (the reference returns it wrapped as "failed to hash data: %w").  Returns RC_NIL, or
+ * RC_ERR_GPU if the engine failed (no digest valid). */
+int32_t rc_hash_batch_with_nonce(rc_cipher *c, uint64_t n, const rc_reader *srcs, const uint8_t *nonces,
+                                 uint8_t *md5, int32_t *errs);
 
 /* Message of an rc_* error value (the reference's error string). */
 const char *rc_error_string(int32_t err);

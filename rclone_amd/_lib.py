@@ -49,10 +49,12 @@ _SIGS = [
     ("xs_keygen_batch_dev", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, vp, u64, vp, u64, vp, u64, vp, vp]),
     ("xs_fill_random_dev", ctypes.c_int, [vp, u64, u64, vp]),
     ("xs_fill_blocks_dev", ctypes.c_int, [vp, u64, u64, u64, u64, vp]),
+    ("xs_md5_batch_dev", ctypes.c_int, [vp, u64, vp, u64, vp, vp, vp]),
     ("xs_engine_create", vp, [ctypes.c_int, ctypes.c_uint32, ctypes.c_int]),
     ("xs_engine_destroy", None, [vp]),
     ("xs_engine_seal", ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, u64, vp, u64, vp]),
     ("xs_engine_open", ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, u64, vp, u64, vp, vp]),
+    ("xs_engine_seal_md5", ctypes.c_int, [vp, ctypes.c_char_p, u64, vp, vp, vp, vp, vp]),
     ("xs_host_alloc", vp, [ctypes.c_size_t]),
     ("xs_host_free", None, [vp]),
     # cipher.go mirror
@@ -80,6 +82,7 @@ _SIGS = [
     ("rc_decrypter_nonce", None, [vp, vp]),
     ("rc_decrypter_wrapped_error", i32, [vp]),
     ("rc_decrypter_free", None, [vp]),
+    ("rc_hash_batch_with_nonce", i32, [vp, u64, vp, vp, vp, vp]),
     ("rc_error_string", ctypes.c_char_p, [i32]),
 ]
 

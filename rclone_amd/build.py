@@ -14,7 +14,7 @@ LIB = os.path.join(HERE, "librclone_crypt.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RCLONE_AMD_ARCH", "gfx950")
 
-SOURCES = ["xs_kernels.hip", "xs_api.cpp", "cipher.cpp", "scrypt.cpp"]
+SOURCES = ["xs_kernels.hip", "xs_md5.hip", "xs_api.cpp", "cipher.cpp", "scrypt.cpp"]
 
 
 def sources():

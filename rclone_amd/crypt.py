@@ -299,6 +299,43 @@ class Cipher:
         """DecryptDataSeek (cipher.go:1112); open_fn(offset, limit) -> reader."""
         return Decrypter(self, None, open_fn=open_fn, offset=offset, limit=limit)
 
+    # ---------------------------------------------------------------- hashes (crypt.go:784-852)
+    def hash_batch_with_nonce(self, items):
+        """Fs.computeHashWithNonce (crypt.go:784) for MD5, batched: items = [(nonce, src)], src a
+        Go-style reader (closed after reading, fs.CheckClose).  Sealing and MD5 both run on the
+        GPU (rc_hash_batch_with_nonce); returns per item the 16-byte digest, or the exception
+        the source raised (the reference wraps it: "failed to hash data: %w")."""
+        n = len(items)
+        if n == 0:
+            return []
+        nonces = b"".join(bytes(nc) for nc, _ in items)
+        if len(nonces) != 24 * n:
+            raise ValueError("nonces must be 24 bytes")
+        bridges = [_ReaderBridge(src, closer=True) for _, src in items]
+        arr = (_lib.RcReader * n)(*[b.c for b in bridges])
+        md5 = ctypes.create_string_buffer(16 * n)
+        errs = (ctypes.c_int32 * n)()
+        _raise(_lib.lib().rc_hash_batch_with_nonce(self._h, n, arr, nonces, md5, errs))
+        out = []
+        for i in range(n):
+            out.append(md5.raw[16 * i:16 * i + 16] if errs[i] == RC_NIL else _ERRS.exc(errs[i]))
+        return out
+
+    def compute_hash_with_nonce(self, nonce: bytes, src) -> str:
+        """computeHashWithNonce (crypt.go:784): MD5 hex of src encrypted with nonce."""
+        r = self.hash_batch_with_nonce([(nonce, src)])[0]
+        if isinstance(r, BaseException):
+            raise r
+        return r.hex()
+
+    def compute_hash(self, obj, src) -> str:
+        """ComputeHash (crypt.go:816): the nonce comes from the encrypted object's header (read
+        with newDecrypter, then closed), then computeHashWithNonce over src."""
+        d = self.decrypt_data(obj)
+        nonce = d.nonce
+        d.close()
+        return self.compute_hash_with_nonce(nonce, src)
+
 
 class Encrypter:
     """encrypter (cipher.go:681): an io.Reader of the encrypted stream."""

@@ -86,6 +86,19 @@ struct PinnedBuf {
     n = p ? bytes : 0;
     return p != nullptr;
   }
+  // grow keeping the contents (doubling)
+  bool ensure_keep(size_t bytes) {
+    if (n >= bytes) return true;
+    size_t cap = n ? n : (1u << 20);
+    while (cap < bytes) cap *= 2;
+    uint8_t* q = (uint8_t*)xs_host_alloc(cap);
+    if (!q) return false;
+    if (p) memcpy(q, p, n);
+    xs_host_free(p);
+    p = q;
+    n = cap;
+    return true;
+  }
   void release() {
     xs_host_free(p);
     p = nullptr;
@@ -683,3 +696,48 @@ extern "C" int32_t rc_decrypter_close(rc_decrypter* fh) {
 extern "C" void rc_decrypter_nonce(const rc_decrypter* fh, uint8_t out[24]) { memcpy(out, fh->nonce, 24); }
 extern "C" int32_t rc_decrypter_wrapped_error(const rc_decrypter* fh) { return fh->wrapped; }
 extern "C" void rc_decrypter_free(rc_decrypter* fh) { delete fh; }
+
+// ---------------------------------------------------------------- computeHashWithNonce, batched
+extern "C" int32_t rc_hash_batch_with_nonce(rc_cipher* c, uint64_t n, const rc_reader* srcs, const uint8_t* nonces,
+                                            uint8_t* md5, int32_t* errs) {
+  if (n == 0) return RC_NIL;
+  if (!c || !srcs || !nonces || !md5 || !errs) return RC_ERR_INVALID;
+  xs_engine* e = engine();
+  if (!e) return RC_ERR_GPU;
+  PinnedBuf buf;
+  uint64_t pos = 0;
+  std::vector<uint64_t> offs, lens;
+  std::vector<uint8_t> ns;
+  std::vector<uint64_t> idx;  // objects that read cleanly
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t start = (pos + 15) & ~15ull;
+    pos = start;
+    int32_t err = RC_NIL;
+    for (;;) {
+      if (!buf.ensure_keep(pos + kBlockData)) return RC_ERR_GPU;
+      int64_t got = read_fill(srcs[i], buf.p + pos, kBlockData, &err);
+      pos += (uint64_t)got;
+      if (err != RC_NIL) break;
+    }
+    if (err == RC_EOF) err = RC_NIL;  // io.Copy: EOF is success
+    if (srcs[i].close) {              // defer fs.CheckClose(in, &err)
+      int32_t ce = srcs[i].close(srcs[i].user);
+      if (err == RC_NIL && ce != RC_NIL) err = ce;
+    }
+    errs[i] = err;
+    if (err != RC_NIL) {
+      pos = start;  // drop the partial object
+      continue;
+    }
+    offs.push_back(start);
+    lens.push_back(pos - start);
+    ns.insert(ns.end(), nonces + 24 * i, nonces + 24 * i + 24);
+    idx.push_back(i);
+  }
+  if (idx.empty()) return RC_NIL;
+  std::vector<uint8_t> dig(16 * idx.size());
+  if (xs_engine_seal_md5(e, c->data_key, idx.size(), ns.data(), offs.data(), lens.data(), buf.p, dig.data()) != XS_OK)
+    return RC_ERR_GPU;
+  for (size_t k = 0; k < idx.size(); k++) memcpy(md5 + 16 * idx[k], dig.data() + 16 * k, 16);
+  return RC_NIL;
+}

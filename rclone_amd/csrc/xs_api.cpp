@@ -7,6 +7,7 @@
 // overlap (the host-path number in DESIGN.md).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -217,6 +218,18 @@ int xs_fill_random_dev(void* d, uint64_t nbytes, uint64_t seed, void* stream) {
   return XS_OK;
 }
 
+int xs_md5_batch_dev(const xs_md5_desc* d_desc, uint64_t n, const void* d_src, uint64_t src_len, uint8_t* d_digest,
+                     uint8_t* d_ok, void* stream) {
+  if (n == 0) return XS_OK;
+  if (!d_desc || !d_digest || (!d_src && src_len)) {
+    set_error("xs_md5_batch_dev: null argument");
+    return XS_ERR_INVALID;
+  }
+  hipError_t e = launch_md5(d_desc, n, (const uint8_t*)d_src, src_len, d_digest, d_ok, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "md5 launch");
+  return XS_OK;
+}
+
 int xs_fill_blocks_dev(void* d, uint64_t nblocks, uint64_t first_block, uint64_t block_stride, uint64_t seed,
                        void* stream) {
   if (!d || !aligned16(d) || block_stride == 0) {
@@ -256,7 +269,27 @@ struct xs_engine {
     uint8_t* d_ok = nullptr;
   };
   std::vector<Slot> slots;
+  // grow-only buffers of xs_engine_seal_md5 (whole objects per group)
+  struct HashBufs {
+    uint8_t* d_plain = nullptr;
+    uint8_t* d_body = nullptr;
+    uint8_t* d_desc = nullptr;
+    uint8_t* d_mdesc = nullptr;
+    uint8_t* d_digest = nullptr;
+    BlockKey* d_keys = nullptr;
+    size_t plain_cap = 0, body_cap = 0, desc_cap = 0, mdesc_cap = 0, digest_cap = 0, keys_cap = 0;
+  } hb;
 };
+
+static bool grow(uint8_t** p, size_t* cap, size_t need) {
+  if (*cap >= need) return true;
+  (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (hipMalloc(p, need ? need : 16) != hipSuccess) return false;
+  *cap = need;
+  return true;
+}
 
 static void engine_free(xs_engine* e) {
   if (!e) return;
@@ -269,6 +302,12 @@ static void engine_free(xs_engine* e) {
     (void)hipFree(sl.d_ok);
     if (sl.s) (void)hipStreamDestroy(sl.s);
   }
+  (void)hipFree(e->hb.d_plain);
+  (void)hipFree(e->hb.d_body);
+  (void)hipFree(e->hb.d_desc);
+  (void)hipFree(e->hb.d_mdesc);
+  (void)hipFree(e->hb.d_digest);
+  (void)hipFree(e->hb.d_keys);
   delete e;
 }
 
@@ -376,4 +415,123 @@ extern "C" int xs_engine_open(xs_engine* e, const uint8_t key[32], const uint8_t
     if (err != hipSuccess) return hip_fail(err, "D2H ok");
   }
   return engine_sync(e);
+}
+
+// ---------------------------------------------------------------- seal + MD5 (cryptcheck)
+static NonceArg bounds_arg(uint64_t src_len, uint64_t dst_len) {  // descriptor-mode keygen bounds
+  NonceArg b{};
+  b.n[0] = (uint32_t)src_len; b.n[1] = (uint32_t)(src_len >> 32);
+  b.n[2] = (uint32_t)dst_len; b.n[3] = (uint32_t)(dst_len >> 32);
+  return b;  // hipMalloc buffers: base alignment bits 0
+}
+
+static void nonce_add_host(uint8_t n[24], uint64_t x) {  // nonce.add (cipher.go:665-678)
+  uint64_t carry = 0;
+  for (int i = 0; i < 8; i++) {
+    const uint64_t sum = (uint64_t)n[i] + (uint8_t)(x >> (8 * i)) + carry;
+    n[i] = (uint8_t)sum;
+    carry = sum >> 8;
+  }
+  for (int i = 8; i < 24 && carry; i++) {
+    const uint64_t sum = (uint64_t)n[i] + carry;
+    n[i] = (uint8_t)sum;
+    carry = sum >> 8;
+  }
+}
+
+static uint64_t body_bytes(uint64_t plain_len) {
+  const uint64_t nb = (plain_len + XS_BLOCK_DATA - 1) / XS_BLOCK_DATA;
+  return plain_len + nb * XS_BLOCK_HDR;
+}
+
+extern "C" int xs_engine_seal_md5(xs_engine* e, const uint8_t key[32], uint64_t nobj, const uint8_t* nonces,
+                                  const uint64_t* offs, const uint64_t* lens, const void* plain, uint8_t* md5) {
+  if (nobj == 0) return XS_OK;
+  if (!e || !key || !nonces || !offs || !lens || !md5) {
+    set_error("xs_engine_seal_md5: null argument");
+    return XS_ERR_INVALID;
+  }
+  for (uint64_t i = 0; i < nobj; i++) {
+    if ((offs[i] & 15u) || (lens[i] && !plain)) {
+      set_error("xs_engine_seal_md5: object %llu: plaintext offset must be 16-byte aligned",
+                (unsigned long long)i);
+      return XS_ERR_INVALID;
+    }
+  }
+  static const uint8_t magic[8] = {'R', 'C', 'L', 'O', 'N', 'E', 0, 0};
+  std::lock_guard<std::mutex> g(e->mu);
+  if (hipSetDevice(e->device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
+  hipStream_t st = e->slots[0].s;
+  auto& hb = e->hb;
+  // groups of whole objects, ~budget plaintext bytes each (MD5 is sequential per object)
+  const uint64_t budget = std::max<uint64_t>((uint64_t)e->batch * XS_BLOCK_DATA * 16, 256ull << 20);
+  std::vector<xs_block_desc> desc;
+  std::vector<xs_md5_desc> mdesc;
+  uint64_t o0 = 0;
+  while (o0 < nobj) {
+    uint64_t o1 = o0, lo = UINT64_MAX, hi = 0, bsum = 0, nblk = 0;
+    while (o1 < nobj) {
+      const uint64_t nlo = std::min(lo, offs[o1]), nhi = std::max(hi, offs[o1] + lens[o1]);
+      if (o1 > o0 && nhi - nlo > budget) break;
+      lo = nlo;
+      hi = nhi;
+      bsum += (body_bytes(lens[o1]) + 15) & ~15ull;
+      nblk += (lens[o1] + XS_BLOCK_DATA - 1) / XS_BLOCK_DATA;
+      o1++;
+    }
+    const uint64_t span = hi > lo ? hi - lo : 0, ng = o1 - o0;
+    desc.clear();
+    mdesc.assign(ng, xs_md5_desc{});
+    uint64_t w = 0;
+    for (uint64_t i = o0; i < o1; i++) {
+      const uint64_t nb = (lens[i] + XS_BLOCK_DATA - 1) / XS_BLOCK_DATA;
+      xs_md5_desc& m = mdesc[i - o0];
+      m.off = w;
+      m.len = body_bytes(lens[i]);
+      memcpy(m.prefix, magic, 8);
+      memcpy(m.prefix + 8, nonces + 24 * i, 24);
+      m.prefix_len = 32;
+      for (uint64_t j = 0; j < nb; j++) {
+        xs_block_desc d{};
+        d.src_off = offs[i] - lo + j * XS_BLOCK_DATA;
+        d.dst_off = w + j * XS_BLOCK_SIZE;
+        const uint64_t rem = lens[i] - j * XS_BLOCK_DATA;
+        d.len = (uint32_t)(rem < (uint64_t)XS_BLOCK_DATA ? rem : XS_BLOCK_DATA);
+        memcpy(d.nonce, nonces + 24 * i, 24);
+        nonce_add_host(d.nonce, j);
+        desc.push_back(d);
+      }
+      w += (m.len + 15) & ~15ull;
+    }
+    if (!grow(&hb.d_plain, &hb.plain_cap, span) || !grow(&hb.d_body, &hb.body_cap, bsum) ||
+        !grow(&hb.d_desc, &hb.desc_cap, nblk * sizeof(xs_block_desc)) ||
+        !grow(&hb.d_mdesc, &hb.mdesc_cap, ng * sizeof(xs_md5_desc)) || !grow(&hb.d_digest, &hb.digest_cap, ng * 16) ||
+        !grow((uint8_t**)&hb.d_keys, &hb.keys_cap, nblk * sizeof(BlockKey))) {
+      set_error("xs_engine_seal_md5: device allocation failed");
+      return XS_ERR_HIP;
+    }
+    hipError_t err = hipSuccess;
+    if (span) err = hipMemcpyAsync(hb.d_plain, (const uint8_t*)plain + lo, span, hipMemcpyHostToDevice, st);
+    if (err == hipSuccess && nblk)
+      err = hipMemcpyAsync(hb.d_desc, desc.data(), nblk * sizeof(xs_block_desc), hipMemcpyHostToDevice, st);
+    if (err == hipSuccess)
+      err = hipMemcpyAsync(hb.d_mdesc, mdesc.data(), ng * sizeof(xs_md5_desc), hipMemcpyHostToDevice, st);
+    if (err != hipSuccess) return hip_fail(err, "H2D");
+    if (nblk) {
+      err = launch_keygen(2, key_arg(key), bounds_arg(span, bsum), 0, 0, nblk, (const xs_block_desc*)hb.d_desc,
+                          hb.d_keys, st);
+      if (err != hipSuccess) return hip_fail(err, "keygen");
+      err = launch_crypt(true, hb.d_keys, nblk, hb.d_plain, hb.d_body, nullptr, st);
+      if (err != hipSuccess) return hip_fail(err, "seal");
+    }
+    err = launch_md5((const xs_md5_desc*)hb.d_mdesc, ng, hb.d_body, bsum, hb.d_digest, nullptr, st);
+    if (err != hipSuccess) return hip_fail(err, "md5");
+    err = hipMemcpyAsync(md5 + 16 * o0, hb.d_digest, ng * 16, hipMemcpyDeviceToHost, st);
+    if (err != hipSuccess) return hip_fail(err, "D2H");
+    // the host-side descriptor vectors are reused next group: wait for this group's copies
+    err = hipStreamSynchronize(st);
+    if (err != hipSuccess) return hip_fail(err, "engine stream");
+    o0 = o1;
+  }
+  return XS_OK;
 }

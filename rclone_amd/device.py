@@ -153,3 +153,27 @@ def open_batch(key: bytes, desc, src: torch.Tensor, dst: torch.Tensor, ok: torch
                                       dst.numel(), ok.data_ptr(), ws.data_ptr(), _stream(src))
     _lib.check(rc, "xs_open_batch_dev")
     return ok[:nb]
+
+
+MD5_DESC_BYTES = 64
+
+
+def md5_batch(desc, src: torch.Tensor):
+    """MD5 of many streams in HBM (xs_md5_batch_dev): desc = numpy structured array of
+    xs_md5_desc (off, len, prefix[32], prefix_len) or a uint8 device tensor; returns
+    (digests uint8 [n,16], ok uint8 [n]) on the device."""
+    _require_gpu(src)
+    if isinstance(desc, torch.Tensor):
+        _require_gpu(desc)
+        d = desc
+    else:
+        import numpy as np
+        assert desc.dtype.itemsize == MD5_DESC_BYTES
+        d = torch.from_numpy(np.frombuffer(desc.tobytes(), dtype=np.uint8).copy()).to(src.device)
+    n = d.numel() // MD5_DESC_BYTES
+    dig = torch.empty(max(n, 1) * 16, dtype=torch.uint8, device=src.device)
+    ok = torch.empty(max(n, 1), dtype=torch.uint8, device=src.device)
+    rc = _lib.lib().xs_md5_batch_dev(d.data_ptr(), n, src.data_ptr(), src.numel(), dig.data_ptr(), ok.data_ptr(),
+                                     _stream(src))
+    _lib.check(rc, "xs_md5_batch_dev")
+    return dig[:n * 16].view(-1, 16), ok[:n]
