@@ -14,7 +14,7 @@ struct NonceArg {
   uint32_t n[6];
 };
 
-// Per-block key schedule written by xs_keygen, read by xs_crypt (960 bytes).
+// Per-block key schedule written by xs_keygen, read by xs_crypt (2272 bytes).
 struct __attribute__((aligned(16))) BlockKey {
   uint32_t subkey[8];  // HSalsa20(key, nonce[0:16])
   uint32_t n2[2];      // nonce[16:24] (Salsa20 words 6, 7)
@@ -29,8 +29,12 @@ struct __attribute__((aligned(16))) BlockKey {
   uint32_t pad[2];
   uint32_t T1[32][5];  // r^0 .. r^31
   uint32_t T2[8][5];   // r^(32a), a = 0..7 (a lane's final exponent is < 256)
+  // matrix-core Poly1305 (full blocks only, xs_kernels.hip crypt_block_mfma)
+  uint32_t W[64][5];   // r^(64k), k = 0..63: weight of 64-chunk group g is W[63-g]
+  uint32_t corr[5];    // key-only correction term added once per block
+  uint32_t pad2[3];
 };
-static_assert(sizeof(BlockKey) == 960, "BlockKey layout");
+static_assert(sizeof(BlockKey) == 2272, "BlockKey layout");
 
 hipError_t launch_keygen(int mode, const KeyArg& key, const NonceArg& nonce0, uint64_t first_block,
                          uint64_t total_len, uint64_t nblocks, const xs_block_desc* desc, BlockKey* out,

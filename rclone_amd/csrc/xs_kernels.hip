@@ -409,6 +409,77 @@ __device__ __forceinline__ void ptag(const P5& hc, const uint32_t (&s)[4], uint3
   tag[3] = (uint32_t)f;
 }
 
+// ---------------------------------------------------------------- matrix-core Poly1305 tables
+// Full-block tag as h = sum_g r^(66-g) T_g (+ chunks 4094, 4095), column g = (c+2) mod 64,
+// row p = (c+2) / 64, T_g = sum_p (c_{p,g} + 2^128) W_{63-p}, W_k = r^(64k).  The kernel gets
+// sum_p c_{p,g} W_{63-p} from i8 MFMAs over the ciphertext bytes biased to signed (c - 128),
+// accumulators started at 2^24; corr collects every key-only term:
+//   corr = S * (E * sum_k W_k - B) - 2^128 (r^66 + r^65) W_63,   S = sum_{e=3..66} r^e,
+// E = 128*(1 + 256 + ... + 256^15) + 2^128 (byte bias and pad bit of every row),
+// B = 2^24 * (1 + 256 + ... + 256^31) (accumulator bias).  The key slots (row 0, columns 0
+// and 1) are fed as zero bytes; only their pad bits need removing.
+__device__ __constant__ uint32_t kE[5] = {0x808080u, 0x202020u, 0x80808u, 0x2020202u, 0x1808080u};
+__device__ __constant__ uint32_t kB[5] = {0x242d2d0u, 0x909090u, 0x242424u, 0x1090909u, 0x2424242u};
+
+// a - b mod p (b canonical): a + 4p - b, limbs < 2^29, then normalised
+__device__ __forceinline__ P5 psub(const P5& a, const P5& b) {
+  P5 o;
+  o.v[0] = a.v[0] + 0xFFFFFECu - b.v[0];
+#pragma unroll
+  for (int i = 1; i < 5; i++) o.v[i] = a.v[i] + 0xFFFFFFCu - b.v[i];
+  pnorm(o);
+  return o;
+}
+
+__device__ void mfma_tables(const P5& r, const P5& r32, BlockKey* __restrict__ o) {
+  // S = sum_{e=3..66} r^e, and r^65, r^66
+  P5 pw = pcanon(pmul(pmul(r, r), r));  // r^3
+  P5 S = pw, r65 = pw, r66 = pw;
+  for (int e = 4; e <= 66; e++) {
+    pw = pcanon(pmul(pw, r));
+#pragma unroll
+    for (int i = 0; i < 5; i++) S.v[i] += pw.v[i];
+    if (e == 65) r65 = pw;
+    if (e == 66) r66 = pw;
+    if ((e & 7) == 0) S = pcanon(S);
+  }
+  S = pcanon(S);
+  // W_k = r^(64k), sum_k W_k
+  const P5 r64 = pcanon(pmul(r32, r32));
+  P5 w, SW;
+  w.v[0] = 1; w.v[1] = w.v[2] = w.v[3] = w.v[4] = 0;
+  SW = w;
+#pragma unroll
+  for (int i = 0; i < 5; i++) o->W[0][i] = w.v[i];
+  for (int k = 1; k < 64; k++) {
+    w = pcanon(pmul(w, r64));
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      o->W[k][i] = w.v[i];
+      SW.v[i] += w.v[i];
+    }
+    if ((k & 7) == 0) SW = pcanon(SW);
+  }
+  SW = pcanon(SW);  // w = W_63 now
+  P5 E, B, two128;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    E.v[i] = kE[i];
+    B.v[i] = kB[i];
+    two128.v[i] = 0;
+  }
+  two128.v[4] = 1u << 24;  // 2^128 = 2^(104 + 24)
+  const P5 es_b = pcanon(psub(pcanon(pmul(E, SW)), B));
+  const P5 a = pcanon(pmul(S, es_b));
+  P5 kk = r65;
+#pragma unroll
+  for (int i = 0; i < 5; i++) kk.v[i] += r66.v[i];
+  const P5 b = pcanon(pmul(pmul(two128, pcanon(kk)), w));
+  const P5 c = pcanon(psub(a, b));
+#pragma unroll
+  for (int i = 0; i < 5; i++) o->corr[i] = c.v[i];
+}
+
 // ---------------------------------------------------------------- keygen
 // One lane per crypt block.  MODE: 0 object seal, 1 object open, 2 descriptor seal,
 // 3 descriptor open.  Object mode derives nonce, offsets and length from the block
@@ -532,6 +603,7 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
   P5 R = pcanon(pmul(r224, r29));
 #pragma unroll
   for (int i = 0; i < 5; i++) o->R[i] = R.v[i];
+  if (len == XS_BLOCK_DATA) mfma_tables(r, r32, o);
 }
 
 // ---------------------------------------------------------------- main block kernel
@@ -546,7 +618,15 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
 // keystream is ready, XORed and stored.  Lane 63 also owns chunks 4094, 4095 (keystream block
 // 1024, precomputed by keygen), so every lane's Horner multipliers are uniform: r inside a
 // group, r^253 between groups.
-constexpr int LDS_WORDS = 4 * 1024;
+#ifndef XS_POLY_MFMA
+#define XS_POLY_MFMA 1  // full-block Poly1305 on the matrix cores (0: radix-2^32 VALU Horner)
+#endif
+#if XS_POLY_MFMA
+constexpr int WAVE_LDS_WORDS = 1024 + 768;  // 4 KiB staging + 3 KiB Toeplitz table
+#else
+constexpr int WAVE_LDS_WORDS = 1024;
+#endif
+constexpr int LDS_WORDS = 4 * WAVE_LDS_WORDS;
 constexpr uint32_t LANES = 64, GROUPS = 16;
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -767,6 +847,224 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
   }
 }
 
+// ---------------------------------------------------------------- full blocks on the matrix cores
+// Poly1305 of a full 64 KiB block as i8 GEMMs (algebra: mfma_tables).  Index the
+// message chunks c = -2 .. 4093 by x = c + 2 = 64 p + g: row p (0..63) = one KiB of the
+// keystream, column g (0..63).  Chunk c's Horner exponent is 4096 - c = 64(63-p) + (66-g), so
+//   h = sum_g r^(66-g) * sum_p (c_{p,g} + 2^128) r^(64(63-p))   (+ chunks 4094, 4095).
+// The inner sums for 32 columns at a time are one 32 x 32 i8 MFMA accumulator:
+//   acc[q][g] = 2^24 + sum_p sum_a Wd_p[q - a] * (byte_a(c_{p,g}) - 128)
+// with Wd_p the 17 signed base-256 digits of r^(64(63-p)) (A operand: a Toeplitz window of the
+// wave's LDS table Z) and the ciphertext bytes XOR 0x80 (B operand).  Lanes keep the
+// contiguous Salsa20 mapping (keystream block K = 64u + l in super-iteration u covers rows
+// 4u .. 4u+3, columns 4(l&15) .. +3), so global loads/stores stay 4 KiB-contiguous per wave;
+// the B operands are gathered from the wave's LDS staging slot.  Key slots (x = 0, 1) are fed
+// as zero bytes; the key-only terms are in BlockKey::corr.
+typedef int xs_v4i __attribute__((ext_vector_type(4)));
+typedef int xs_v16i __attribute__((ext_vector_type(16)));
+constexpr int Z_WORDS = 64 * 12;  // 64 rows x 48 bytes
+
+// 275-bit biased column value held by lane pair (n, kh = 0/1) -> residue mod 2^130-5
+__device__ __forceinline__ P5 column_value(const xs_v16i& acc, uint32_t kh) {
+  // acc[i] = byte-position sum for q = (i&3) + 8(i>>2) + 4kh
+  uint64_t sx[4];
+#pragma unroll
+  for (int I = 0; I < 4; I++)
+    sx[I] = (uint64_t)(uint32_t)acc[4 * I] + ((uint64_t)(uint32_t)acc[4 * I + 1] << 8) +
+            ((uint64_t)(uint32_t)acc[4 * I + 2] << 16) + ((uint64_t)(uint32_t)acc[4 * I + 3] << 24);
+  uint64_t x[8];  // weight 2^(32w): word w comes from the lane with kh = w & 1, I = w >> 1
+#pragma unroll
+  for (int I = 0; I < 4; I++) {
+    const uint32_t plo = (uint32_t)__shfl_xor((int)(uint32_t)sx[I], 32, 64);
+    const uint32_t phi = (uint32_t)__shfl_xor((int)(uint32_t)(sx[I] >> 32), 32, 64);
+    const uint64_t px = ((uint64_t)phi << 32) | plo;
+    x[2 * I] = kh ? px : sx[I];
+    x[2 * I + 1] = kh ? sx[I] : px;
+  }
+  uint32_t L[9];
+  uint64_t c = 0;
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    const uint64_t tt = x[w] + c;
+    L[w] = (uint32_t)tt;
+    c = tt >> 32;
+  }
+  L[8] = (uint32_t)c;  // < 2^19: the value is < 2^275
+  uint32_t v[11];
+  v[0] = L[0] & M26;
+  v[1] = alignbit(L[1], L[0], 26) & M26;
+  v[2] = alignbit(L[2], L[1], 20) & M26;
+  v[3] = alignbit(L[3], L[2], 14) & M26;
+  v[4] = alignbit(L[4], L[3], 8) & M26;
+  v[5] = (L[4] >> 2) & M26;
+  v[6] = alignbit(L[5], L[4], 28) & M26;
+  v[7] = alignbit(L[6], L[5], 22) & M26;
+  v[8] = alignbit(L[7], L[6], 16) & M26;
+  v[9] = alignbit(L[8], L[7], 10) & M26;
+  v[10] = L[8] >> 4;
+  v[5] += 5u * v[10];  // 2^260 = 2^130 * 2^130 -> 5 * 2^130
+  P5 V;
+#pragma unroll
+  for (int i = 0; i < 5; i++) V.v[i] = v[i] + 5u * v[i + 5];
+  pnorm(V);
+  return V;
+}
+
+template <bool SEAL>
+__device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk, const uint8_t* __restrict__ pin,
+                                                 uint8_t* __restrict__ pout, uint32_t* wb, uint32_t* zb, P5& h) {
+  const uint32_t l = threadIdx.x & 63u, m = l & 31u, kh = l >> 5;
+  // ---- Z table: row p = l holds the signed digits D_0..D_16 of r^(64(63-p)) reversed,
+  // Z[u] = D_{31-u} for 15 <= u <= 31, zero elsewhere (12 words per row).
+  {
+    uint32_t q[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) q[i] = bk->W[63u - l][i];  // canonical
+    uint32_t w0 = q[0] | (q[1] << 26), w1 = (q[1] >> 6) | (q[2] << 20), w2 = (q[2] >> 12) | (q[3] << 14),
+             w3 = (q[3] >> 18) | (q[4] << 8), w4 = q[4] >> 24;
+    unsigned cy;  // +0x80 in every byte, carried; flipping each byte's top bit then gives digits in [-128, 127]
+    w0 = __builtin_addc(w0, 0x80808080u, 0u, &cy);
+    w1 = __builtin_addc(w1, 0x80808080u, cy, &cy);
+    w2 = __builtin_addc(w2, 0x80808080u, cy, &cy);
+    w3 = __builtin_addc(w3, 0x80808080u, cy, &cy);
+    w4 = (w4 + 0x80u + cy) ^ 0x80u;
+    w0 ^= 0x80808080u;
+    w1 ^= 0x80808080u;
+    w2 ^= 0x80808080u;
+    w3 ^= 0x80808080u;
+    uint4* row = reinterpret_cast<uint4*>(zb + 12u * l);
+    row[0] = make_uint4(0u, 0u, 0u, w4 << 24);
+    row[1] = make_uint4(__builtin_bswap32(w3), __builtin_bswap32(w2), __builtin_bswap32(w1), __builtin_bswap32(w0));
+    row[2] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  uint32_t k[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) k[i] = bk->subkey[i];
+  const SalsaPre pre = salsa_pre(k, bk->n2[0], bk->n2[1]);
+  const uint32_t zoff = (31u - m) >> 2, zsh = (31u - m) & 3u;
+  // B gather: column g = 32 nt + m of row 4u + 2jr + kh lives in lane 16(2jr + kh) + 8nt + (m >> 2),
+  // chunk slot m & 3, of the staging slot (layout [slot][lane], 16 bytes each)
+  const uint32_t* bsrc = wb + 256u * (m & 3u) + 4u * (16u * kh + (m >> 2));
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own Z writes are visible
+  xs_v16i acc0, acc1;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    acc0[i] = 1 << 24;
+    acc1[i] = 1 << 24;
+  }
+#pragma unroll 1
+  for (int u = 0; u < 16; u++) {
+    const uint32_t K = 64u * u + l;
+    const bool key_slots = K == 0u;  // chunks -2, -1: the Poly1305 key, not message
+    const uint8_t* src = pin + 64u * K - 32u;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (j >= 2 || !key_slots) __builtin_amdgcn_global_load_lds(src + 16 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
+    uint32_t ks[16];
+    salsa20_block_pre(pre, K, ks);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t d[16];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint4 v = *reinterpret_cast<const uint4*>(wb + 256 * j + 4 * l);
+      d[4 * j] = v.x; d[4 * j + 1] = v.y; d[4 * j + 2] = v.z; d[4 * j + 3] = v.w;
+    }
+    uint32_t o[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) o[i] = d[i] ^ ks[i];
+    uint8_t* dst = pout + 64u * K - 32u;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (j >= 2 || !key_slots)
+        *reinterpret_cast<uint4*>(dst + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
+    // the ciphertext must be in the staging slot for the gather: seal writes o over d; the
+    // key slots become zero bytes (for open only they need rewriting)
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const bool z = key_slots && j < 2;
+      if (SEAL || z)
+        *reinterpret_cast<uint4*>(wb + 256 * j + 4 * l) =
+            z ? make_uint4(0u, 0u, 0u, 0u) : make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int jr = 0; jr < 2; jr++) {
+      // A: Toeplitz window of row 4u + 2jr + kh
+      const uint32_t* zr = zb + 12u * (4u * u + 2u * jr + kh) + zoff;
+      const uint32_t z0 = zr[0], z1 = zr[1], z2 = zr[2], z3 = zr[3], z4 = zr[4];
+      xs_v4i A;
+      A[0] = (int)__builtin_amdgcn_alignbyte(z1, z0, zsh);
+      A[1] = (int)__builtin_amdgcn_alignbyte(z2, z1, zsh);
+      A[2] = (int)__builtin_amdgcn_alignbyte(z3, z2, zsh);
+      A[3] = (int)__builtin_amdgcn_alignbyte(z4, z3, zsh);
+#pragma unroll
+      for (int nt = 0; nt < 2; nt++) {
+        const uint4 bv = *reinterpret_cast<const uint4*>(bsrc + 4u * (32u * jr + 8u * nt));
+        xs_v4i B;
+        B[0] = (int)(bv.x ^ 0x80808080u);
+        B[1] = (int)(bv.y ^ 0x80808080u);
+        B[2] = (int)(bv.z ^ 0x80808080u);
+        B[3] = (int)(bv.w ^ 0x80808080u);
+#ifdef XS_ABLATE_NOMFMA  // diagnostic: operand traffic without the matrix op (wrong tags)
+        if (nt == 0) acc0[jr] ^= A[0] ^ A[1] ^ A[2] ^ A[3] ^ B[0] ^ B[1] ^ B[2] ^ B[3];
+        else acc1[jr] ^= A[0] ^ A[1] ^ A[2] ^ A[3] ^ B[0] ^ B[1] ^ B[2] ^ B[3];
+#else
+        if (nt == 0) acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, acc0, 0, 0, 0);
+        else acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, acc1, 0, 0, 0);
+#endif
+      }
+    }
+  }
+  // ---- columns: value mod p times the column weight r^(66-g), summed once per column
+  P5 hs;
+  hs.v[0] = hs.v[1] = hs.v[2] = hs.v[3] = hs.v[4] = 0;
+#pragma unroll
+  for (int nt = 0; nt < 2; nt++) {
+    const P5 V = column_value(nt ? acc1 : acc0, kh);
+    const uint32_t e = 66u - (32u * nt + m);
+    P5 t1, t2;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      t1.v[i] = bk->T1[e & 31u][i];
+      t2.v[i] = bk->T2[e >> 5][i];
+    }
+    const P5 pr = pmul(V, pcanon(pmul(t2, t1)));
+#pragma unroll
+    for (int i = 0; i < 5; i++) hs.v[i] += pr.v[i];
+  }
+  if (kh) hs.v[0] = hs.v[1] = hs.v[2] = hs.v[3] = hs.v[4] = 0;  // each column counted once
+  if (l == 0u) {
+#pragma unroll
+    for (int i = 0; i < 5; i++) hs.v[i] += bk->corr[i];
+  }
+  // chunks 4094, 4095 (keystream block 1024 words 0..7): exponents 2 and 1
+  if (l == 63u) {
+    P5 rr, tl;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      rr.v[i] = bk->r[i];
+      tl.v[i] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const uint32_t off = 16u * (4094u + j);
+      const uint4 v = *reinterpret_cast<const uint4*>(pin + off);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      uint32_t o4[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) o4[i] = w[i] ^ bk->ks1024[4 * j + i];
+      *reinterpret_cast<uint4*>(pout + off) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+      const uint32_t* cw = SEAL ? o4 : w;
+      padd_full(tl, cw[0], cw[1], cw[2], cw[3]);
+      tl = pmul(tl, rr);
+    }
+#pragma unroll
+    for (int i = 0; i < 5; i++) hs.v[i] += tl.v[i];
+  }
+  pnorm(hs);
+  h = hs;
+}
+
 template <bool SEAL>
 __device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, uint64_t nblocks,
                                            const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
@@ -785,11 +1083,15 @@ __device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, ui
   uint8_t* out = dst + bk->dst;
   const uint8_t* pin = SEAL ? in : in + XS_BLOCK_HDR;
   uint8_t* pout = SEAL ? out + XS_BLOCK_HDR : out;
-  uint32_t* wb = lds + wave * 1024u;
+  uint32_t* wb = lds + wave * WAVE_LDS_WORDS;
 
   P5 h;
   h.v[0] = h.v[1] = h.v[2] = h.v[3] = h.v[4] = 0;
+#if XS_POLY_MFMA
+  if (n == XS_BLOCK_DATA) crypt_block_mfma<SEAL>(bk, pin, pout, wb, wb + 1024, h);
+#else
   if (n == XS_BLOCK_DATA) crypt_block<SEAL, true>(bk, pin, pout, n, wb, h);
+#endif
   else crypt_block<SEAL, false>(bk, pin, pout, n, wb, h);
 
   // sum the 64 partials with wave shuffles (limbs < 2^26+2^6 -> < 2^32 after 5 levels)

@@ -11,7 +11,7 @@ int main(int argc, char** argv) {
   const uint64_t nb = 100000;
   uint8_t *plain, *body; xs::BlockKey* ws;
   (void)hipMalloc(&plain, nb * 65536); (void)hipMalloc(&body, nb * 65552); (void)hipMalloc(&ws, nb * sizeof(xs::BlockKey));
-  (void)xs::launch_fill(reinterpret_cast<uint64_t*>(plain), nb * 65536 / 8, 12345, 0);  // random, like bench.py
+  (void)xs::launch_fill(reinterpret_cast<uint64_t*>(plain), nb * 65536 / 8, 12345, 0, 1, 0);  // random, like bench.py
   xs::KeyArg k{}; xs::NonceArg n{};
   for (int i = 0; i < 8; i++) k.k[i] = 0x01020304u * (i + 1);
   uint8_t* okb; xs::BlockKey* ws2; uint8_t* out;
