@@ -852,35 +852,20 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
 // message chunks c = -2 .. 4093 by x = c + 2 = 64 p + g: row p (0..63) = one KiB of the
 // keystream, column g (0..63).  Chunk c's Horner exponent is 4096 - c = 64(63-p) + (66-g), so
 //   h = sum_g r^(66-g) * sum_p (c_{p,g} + 2^128) r^(64(63-p))   (+ chunks 4094, 4095).
-// The inner sums for 32 columns at a time are one 32 x 32 i8 MFMA accumulator:
-//   acc[q][g] = 2^24 + sum_p sum_a Wd_p[q - a] * (byte_a(c_{p,g}) - 128)
-// with Wd_p the 17 signed base-256 digits of r^(64(63-p)) (A operand: a Toeplitz window of the
-// wave's LDS table Z) and the ciphertext bytes XOR 0x80 (B operand).  Lanes keep the
-// contiguous Salsa20 mapping (keystream block K = 64u + l in super-iteration u covers rows
-// 4u .. 4u+3, columns 4(l&15) .. +3), so global loads/stores stay 4 KiB-contiguous per wave;
-// the B operands are gathered from the wave's LDS staging slot.  Key slots (x = 0, 1) are fed
-// as zero bytes; the key-only terms are in BlockKey::corr.
+// In super-iteration u lane l runs keystream block K = 64u + l (4 KiB contiguous per wave),
+// whose chunks j = 0..3 are row 4u + (l>>4), columns 4(l&15) + j.  That is exactly the
+// B-operand layout of v_mfma_i32_16x16x64_i8 (lane l: column l&15, K-group l>>4), so with
+// one accumulator per (chunk j, output half mt)
+//   acc[j][mt][q][n] = 2^24 + sum_p sum_a Wd_p[16mt + q - a] * (byte_a(c_{p, 4n+j}) - 128)
+// the ciphertext never leaves the lane; Wd_p = the 17 signed base-256 digits of r^(64(63-p))
+// (A operand: a Toeplitz window of the wave's LDS table Z, K-group kg <-> row 4u + kg).  Key
+// slots (x = 0, 1) are fed as zero bytes; the key-only terms are in BlockKey::corr.
 typedef int xs_v4i __attribute__((ext_vector_type(4)));
-typedef int xs_v16i __attribute__((ext_vector_type(16)));
 constexpr int Z_WORDS = 64 * 12;  // 64 rows x 48 bytes
 
-// 275-bit biased column value held by lane pair (n, kh = 0/1) -> residue mod 2^130-5
-__device__ __forceinline__ P5 column_value(const xs_v16i& acc, uint32_t kh) {
-  // acc[i] = byte-position sum for q = (i&3) + 8(i>>2) + 4kh
-  uint64_t sx[4];
-#pragma unroll
-  for (int I = 0; I < 4; I++)
-    sx[I] = (uint64_t)(uint32_t)acc[4 * I] + ((uint64_t)(uint32_t)acc[4 * I + 1] << 8) +
-            ((uint64_t)(uint32_t)acc[4 * I + 2] << 16) + ((uint64_t)(uint32_t)acc[4 * I + 3] << 24);
-  uint64_t x[8];  // weight 2^(32w): word w comes from the lane with kh = w & 1, I = w >> 1
-#pragma unroll
-  for (int I = 0; I < 4; I++) {
-    const uint32_t plo = (uint32_t)__shfl_xor((int)(uint32_t)sx[I], 32, 64);
-    const uint32_t phi = (uint32_t)__shfl_xor((int)(uint32_t)(sx[I] >> 32), 32, 64);
-    const uint64_t px = ((uint64_t)phi << 32) | plo;
-    x[2 * I] = kh ? px : sx[I];
-    x[2 * I + 1] = kh ? sx[I] : px;
-  }
+// Column value from its eight 64-bit partial words X[w] (weight 2^(32w), each < 2^50),
+// reduced mod 2^130-5 (limbs < 2^26 + 2^6).
+__device__ __forceinline__ P5 column_value(const uint64_t (&x)[8]) {
   uint32_t L[9];
   uint64_t c = 0;
 #pragma unroll
@@ -913,7 +898,7 @@ __device__ __forceinline__ P5 column_value(const xs_v16i& acc, uint32_t kh) {
 template <bool SEAL>
 __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk, const uint8_t* __restrict__ pin,
                                                  uint8_t* __restrict__ pout, uint32_t* wb, uint32_t* zb, P5& h) {
-  const uint32_t l = threadIdx.x & 63u, m = l & 31u, kh = l >> 5;
+  const uint32_t l = threadIdx.x & 63u, n = l & 15u, kg = l >> 4;
   // ---- Z table: row p = l holds the signed digits D_0..D_16 of r^(64(63-p)) reversed,
   // Z[u] = D_{31-u} for 15 <= u <= 31, zero elsewhere (12 words per row).
   {
@@ -941,17 +926,17 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
 #pragma unroll
   for (int i = 0; i < 8; i++) k[i] = bk->subkey[i];
   const SalsaPre pre = salsa_pre(k, bk->n2[0], bk->n2[1]);
-  const uint32_t zoff = (31u - m) >> 2, zsh = (31u - m) & 3u;
-  // B gather: column g = 32 nt + m of row 4u + 2jr + kh lives in lane 16(2jr + kh) + 8nt + (m >> 2),
-  // chunk slot m & 3, of the staging slot (layout [slot][lane], 16 bytes each)
-  const uint32_t* bsrc = wb + 256u * (m & 3u) + 4u * (16u * kh + (m >> 2));
+  // A window for output q = 16mt + n starts at Z byte 31 - q: words zlo .. zlo + 8 cover both
+  // halves (mt = 1 at word zlo, mt = 0 at word zlo + 4), byte shift zsh
+  const uint32_t zlo = (15u - n) >> 2, zsh = (31u - n) & 3u;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own Z writes are visible
-  xs_v16i acc0, acc1;
+  xs_v4i acc[4][2];
 #pragma unroll
-  for (int i = 0; i < 16; i++) {
-    acc0[i] = 1 << 24;
-    acc1[i] = 1 << 24;
-  }
+  for (int j = 0; j < 4; j++)
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[j][mt][i] = 1 << 24;
 #pragma unroll 1
   for (int u = 0; u < 16; u++) {
     const uint32_t K = 64u * u + l;
@@ -977,62 +962,63 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
     for (int j = 0; j < 4; j++)
       if (j >= 2 || !key_slots)
         *reinterpret_cast<uint4*>(dst + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
-    // the ciphertext must be in the staging slot for the gather: seal writes o over d; the
-    // key slots become zero bytes (for open only they need rewriting)
+    // A operands of row 4u + kg for both output halves
+    const uint32_t* zr = zb + 12u * (4u * u + kg) + zlo;
+    uint32_t z[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) z[i] = zr[i];
+    xs_v4i A[2];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      A[1][i] = (int)__builtin_amdgcn_alignbyte(z[i + 1], z[i], zsh);
+      A[0][i] = (int)__builtin_amdgcn_alignbyte(z[i + 5], z[i + 4], zsh);
+    }
+    const uint32_t* cw = SEAL ? o : d;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const bool z = key_slots && j < 2;
-      if (SEAL || z)
-        *reinterpret_cast<uint4*>(wb + 256 * j + 4 * l) =
-            z ? make_uint4(0u, 0u, 0u, 0u) : make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const bool zero = key_slots && j < 2;
+      xs_v4i B;
 #pragma unroll
-    for (int jr = 0; jr < 2; jr++) {
-      // A: Toeplitz window of row 4u + 2jr + kh
-      const uint32_t* zr = zb + 12u * (4u * u + 2u * jr + kh) + zoff;
-      const uint32_t z0 = zr[0], z1 = zr[1], z2 = zr[2], z3 = zr[3], z4 = zr[4];
-      xs_v4i A;
-      A[0] = (int)__builtin_amdgcn_alignbyte(z1, z0, zsh);
-      A[1] = (int)__builtin_amdgcn_alignbyte(z2, z1, zsh);
-      A[2] = (int)__builtin_amdgcn_alignbyte(z3, z2, zsh);
-      A[3] = (int)__builtin_amdgcn_alignbyte(z4, z3, zsh);
+      for (int i = 0; i < 4; i++) B[i] = (int)(zero ? 0x80808080u : (cw[4 * j + i] ^ 0x80808080u));
 #pragma unroll
-      for (int nt = 0; nt < 2; nt++) {
-        const uint4 bv = *reinterpret_cast<const uint4*>(bsrc + 4u * (32u * jr + 8u * nt));
-        xs_v4i B;
-        B[0] = (int)(bv.x ^ 0x80808080u);
-        B[1] = (int)(bv.y ^ 0x80808080u);
-        B[2] = (int)(bv.z ^ 0x80808080u);
-        B[3] = (int)(bv.w ^ 0x80808080u);
-#ifdef XS_ABLATE_NOMFMA  // diagnostic: operand traffic without the matrix op (wrong tags)
-        if (nt == 0) acc0[jr] ^= A[0] ^ A[1] ^ A[2] ^ A[3] ^ B[0] ^ B[1] ^ B[2] ^ B[3];
-        else acc1[jr] ^= A[0] ^ A[1] ^ A[2] ^ A[3] ^ B[0] ^ B[1] ^ B[2] ^ B[3];
-#else
-        if (nt == 0) acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, acc0, 0, 0, 0);
-        else acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, acc1, 0, 0, 0);
-#endif
-      }
+      for (int mt = 0; mt < 2; mt++) acc[j][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[mt], B, acc[j][mt], 0, 0, 0);
     }
   }
-  // ---- columns: value mod p times the column weight r^(66-g), summed once per column
-  P5 hs;
-  hs.v[0] = hs.v[1] = hs.v[2] = hs.v[3] = hs.v[4] = 0;
+  // ---- transpose the partial words through the (now free) staging slot: lane (n, kg) holds,
+  // for column 4n + j, the words at 2^(32(4mt + kg)); lane λ finalises column 4(λ&15) + (λ>>4)
+  uint64_t* t64 = reinterpret_cast<uint64_t*>(wb);
 #pragma unroll
-  for (int nt = 0; nt < 2; nt++) {
-    const P5 V = column_value(nt ? acc1 : acc0, kh);
-    const uint32_t e = 66u - (32u * nt + m);
+  for (int j = 0; j < 4; j++) {
+    uint64_t sx[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+      sx[mt] = (uint64_t)(uint32_t)acc[j][mt][0] + ((uint64_t)(uint32_t)acc[j][mt][1] << 8) +
+               ((uint64_t)(uint32_t)acc[j][mt][2] << 16) + ((uint64_t)(uint32_t)acc[j][mt][3] << 24);
+    *reinterpret_cast<ulonglong2*>(t64 + (((n * 4u + j) * 4u + kg) * 2u)) = make_ulonglong2(sx[0], sx[1]);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  uint64_t x[8];
+  {
+    const uint64_t* rd = t64 + (n * 4u + kg) * 8u;  // column 4n + kg: (kg', mt) pairs for kg' = 0..3
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++) {
+      const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(rd + 2 * kk);
+      x[kk] = v.x;      // mt = 0: word kk
+      x[4 + kk] = v.y;  // mt = 1: word 4 + kk
+    }
+  }
+  P5 hs;
+  {
+    const P5 V = column_value(x);
+    const uint32_t e = 66u - (4u * n + kg);  // column g = 4n + kg (this lane's column)
     P5 t1, t2;
 #pragma unroll
     for (int i = 0; i < 5; i++) {
       t1.v[i] = bk->T1[e & 31u][i];
       t2.v[i] = bk->T2[e >> 5][i];
     }
-    const P5 pr = pmul(V, pcanon(pmul(t2, t1)));
-#pragma unroll
-    for (int i = 0; i < 5; i++) hs.v[i] += pr.v[i];
+    hs = pmul(V, pcanon(pmul(t2, t1)));
   }
-  if (kh) hs.v[0] = hs.v[1] = hs.v[2] = hs.v[3] = hs.v[4] = 0;  // each column counted once
   if (l == 0u) {
 #pragma unroll
     for (int i = 0; i < 5; i++) hs.v[i] += bk->corr[i];
