@@ -142,6 +142,13 @@ int xs_engine_open(xs_engine *e, const uint8_t key[32], const uint8_t nonce0[24]
  * pays off for many objects per call (hundreds+), not for one large stream. */
 int xs_engine_seal_md5(xs_engine *e, const uint8_t key[32], uint64_t nobj, const uint8_t *nonces,
                        const uint64_t *offs, const uint64_t *lens, const void *plain, uint8_t *md5);
+/* Cross-caller coalescing (default on; env XS_ENGINE_COALESCE=0 or this call turns it off):
+ * concurrent xs_engine_seal/xs_engine_open callers whose request fits one engine batch are
+ * packed into one combined GPU batch (group commit: the first caller in leads, the others
+ * wait).  Results, errors and per-caller buffers are exactly those of separate calls. */
+void xs_engine_set_coalesce(xs_engine *e, int on);
+/* Cumulative coalescing counters: out[0] combined batches, out[1] requests, out[2] blocks. */
+void xs_engine_stats(xs_engine *e, uint64_t out[3]);
 /* Pinned (page-locked) host memory. */
 void *xs_host_alloc(size_t bytes);
 void xs_host_free(void *p);

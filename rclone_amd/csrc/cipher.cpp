@@ -22,6 +22,7 @@
 #include <cerrno>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -76,31 +77,70 @@ xs_engine* engine() {
   return g_engine;
 }
 
+// Pinned staging pool -- the counterpart of the reference's Cipher.buffers sync.Pool
+// (cipher.go:179, :255-262): handles come and go per object, and hipHostMalloc/hipHostFree
+// cost milliseconds and synchronise the device, so buffers are recycled (best fit by size),
+// keeping at most kPoolBytes cached.
+constexpr size_t kPoolBytes = (size_t)1 << 30;
+std::mutex g_pool_mu;
+std::multimap<size_t, uint8_t*> g_pool;
+size_t g_pool_cached = 0;
+
+uint8_t* pool_get(size_t bytes, size_t* cap) {
+  {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    auto it = g_pool.lower_bound(bytes);
+    if (it != g_pool.end() && it->first <= 2 * bytes + (1u << 20)) {
+      *cap = it->first;
+      uint8_t* p = it->second;
+      g_pool_cached -= it->first;
+      g_pool.erase(it);
+      return p;
+    }
+  }
+  uint8_t* p = (uint8_t*)xs_host_alloc(bytes);
+  *cap = p ? bytes : 0;
+  return p;
+}
+
+void pool_put(uint8_t* p, size_t cap) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    if (g_pool_cached + cap <= kPoolBytes) {
+      g_pool.emplace(cap, p);
+      g_pool_cached += cap;
+      return;
+    }
+  }
+  xs_host_free(p);
+}
+
 struct PinnedBuf {
   uint8_t* p = nullptr;
   size_t n = 0;
   bool ensure(size_t bytes) {
     if (n >= bytes) return true;
-    xs_host_free(p);
-    p = (uint8_t*)xs_host_alloc(bytes);
-    n = p ? bytes : 0;
+    pool_put(p, n);
+    p = pool_get(bytes, &n);
     return p != nullptr;
   }
   // grow keeping the contents (doubling)
   bool ensure_keep(size_t bytes) {
     if (n >= bytes) return true;
-    size_t cap = n ? n : (1u << 20);
-    while (cap < bytes) cap *= 2;
-    uint8_t* q = (uint8_t*)xs_host_alloc(cap);
+    size_t want = n ? n : (1u << 20);
+    while (want < bytes) want *= 2;
+    size_t cap = 0;
+    uint8_t* q = pool_get(want, &cap);
     if (!q) return false;
     if (p) memcpy(q, p, n);
-    xs_host_free(p);
+    pool_put(p, n);
     p = q;
     n = cap;
     return true;
   }
   void release() {
-    xs_host_free(p);
+    pool_put(p, n);
     p = nullptr;
     n = 0;
   }

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -269,6 +270,28 @@ struct xs_engine {
     uint8_t* d_ok = nullptr;
   };
   std::vector<Slot> slots;
+  // ---- cross-caller coalescing (group commit, see engine_submit)
+  struct Req {
+    bool seal;
+    uint8_t key[32];
+    uint8_t nonce0[24];
+    uint64_t first_block, nblocks, in_len, out_len;
+    const uint8_t* in;
+    uint8_t* out;
+    uint8_t* ok;
+    int rc;
+    bool done;
+  };
+  bool coalesce = true;
+  std::mutex qmu;
+  std::condition_variable qcv;
+  std::vector<Req*> queue;
+  bool leader = false;
+  uint8_t *c_in = nullptr, *c_out = nullptr, *c_ok = nullptr, *c_desc = nullptr;
+  BlockKey* c_keys = nullptr;
+  xs_block_desc* h_desc = nullptr;  // pinned
+  uint64_t c_cap_blocks = 0, c_cap_bytes = 0;
+  uint64_t st_batches = 0, st_reqs = 0, st_blocks = 0;
   // grow-only buffers of xs_engine_seal_md5 (whole objects per group)
   struct HashBufs {
     uint8_t* d_plain = nullptr;
@@ -302,6 +325,12 @@ static void engine_free(xs_engine* e) {
     (void)hipFree(sl.d_ok);
     if (sl.s) (void)hipStreamDestroy(sl.s);
   }
+  (void)hipFree(e->c_in);
+  (void)hipFree(e->c_out);
+  (void)hipFree(e->c_ok);
+  (void)hipFree(e->c_desc);
+  (void)hipFree(e->c_keys);
+  (void)hipHostFree(e->h_desc);
   (void)hipFree(e->hb.d_plain);
   (void)hipFree(e->hb.d_body);
   (void)hipFree(e->hb.d_desc);
@@ -338,7 +367,33 @@ extern "C" xs_engine* xs_engine_create(int device, uint32_t batch_blocks, int ns
       return nullptr;
     }
   }
+  // coalescing buffers: one combined batch of up to batch_blocks blocks from many callers
+  // (+16 bytes of alignment slack per block for the per-request 16-byte alignment)
+  e->c_cap_blocks = batch_blocks;
+  e->c_cap_bytes = (uint64_t)batch_blocks * (XS_BLOCK_SIZE + 16);
+  if (hipMalloc(&e->c_in, e->c_cap_bytes) != hipSuccess || hipMalloc(&e->c_out, e->c_cap_bytes) != hipSuccess ||
+      hipMalloc(&e->c_ok, batch_blocks) != hipSuccess ||
+      hipMalloc(&e->c_desc, (size_t)batch_blocks * sizeof(xs_block_desc)) != hipSuccess ||
+      hipMalloc(&e->c_keys, (size_t)batch_blocks * sizeof(BlockKey)) != hipSuccess ||
+      hipHostMalloc(&e->h_desc, (size_t)batch_blocks * sizeof(xs_block_desc), hipHostMallocPortable) != hipSuccess) {
+    set_error("xs_engine_create: device allocation failed");
+    engine_free(e);
+    return nullptr;
+  }
+  if (const char* v = getenv("XS_ENGINE_COALESCE")) e->coalesce = atoi(v) != 0;
   return e;
+}
+
+extern "C" void xs_engine_set_coalesce(xs_engine* e, int on) {
+  if (e) e->coalesce = on != 0;
+}
+
+extern "C" void xs_engine_stats(xs_engine* e, uint64_t out[3]) {
+  if (!e || !out) return;
+  std::lock_guard<std::mutex> g(e->qmu);
+  out[0] = e->st_batches;
+  out[1] = e->st_reqs;
+  out[2] = e->st_blocks;
 }
 
 extern "C" void xs_engine_destroy(xs_engine* e) { engine_free(e); }
@@ -352,12 +407,29 @@ static int engine_sync(xs_engine* e) {
   return rc;
 }
 
+static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                         const void* in, uint64_t in_len, void* out, uint8_t* ok, uint64_t nblocks);
+
+static int engine_seal_direct(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                              const void* plain, uint64_t plain_len, void* body);
+static int engine_open_direct(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                              const void* body, uint64_t body_len, void* plain, uint8_t* ok);
+
 extern "C" int xs_engine_seal(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
                               const void* plain, uint64_t plain_len, void* body) {
   if (!e || !key || !nonce0 || (plain_len && (!plain || !body))) {
     set_error("xs_engine_seal: null argument");
     return XS_ERR_INVALID;
   }
+  if (plain_len == 0) return XS_OK;
+  const uint64_t nblocks = (plain_len + XS_BLOCK_DATA - 1) / XS_BLOCK_DATA;
+  if (e->coalesce && nblocks <= e->c_cap_blocks)
+    return engine_submit(e, true, key, nonce0, first_block, plain, plain_len, body, nullptr, nblocks);
+  return engine_seal_direct(e, key, nonce0, first_block, plain, plain_len, body);
+}
+
+static int engine_seal_direct(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                              const void* plain, uint64_t plain_len, void* body) {
   std::lock_guard<std::mutex> g(e->mu);
   if (hipSetDevice(e->device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
   const KeyArg k = key_arg(key);
@@ -393,6 +465,14 @@ extern "C" int xs_engine_open(xs_engine* e, const uint8_t key[32], const uint8_t
     set_error("xs_engine_open: truncated block header");
     return XS_ERR_INVALID;
   }
+  if (e->coalesce && nblocks <= e->c_cap_blocks)
+    return engine_submit(e, false, key, nonce0, first_block, body, body_len, plain, ok, nblocks);
+  return engine_open_direct(e, key, nonce0, first_block, body, body_len, plain, ok);
+}
+
+static int engine_open_direct(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                              const void* body, uint64_t body_len, void* plain, uint8_t* ok) {
+  const uint64_t nblocks = (body_len + XS_BLOCK_SIZE - 1) / XS_BLOCK_SIZE;
   std::lock_guard<std::mutex> g(e->mu);
   if (hipSetDevice(e->device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
   const KeyArg k = key_arg(key);
@@ -415,6 +495,155 @@ extern "C" int xs_engine_open(xs_engine* e, const uint8_t key[32], const uint8_t
     if (err != hipSuccess) return hip_fail(err, "D2H ok");
   }
   return engine_sync(e);
+}
+
+// ---------------------------------------------------------------- cross-caller coalescing
+// rclone runs many transfers/checkers at once (--transfers, --checkers), each handle sealing
+// or opening a few blocks at a time (cipher.go:719-745, :862-898).  Instead of one GPU round
+// trip per handle, callers queue their requests and the first one in becomes the leader: it
+// packs every queued request (up to the engine's batch capacity) into ONE descriptor batch --
+// per-request H2D straight from the caller's buffer, one keygen per (direction, key), one crypt
+// launch per direction, per-request D2H -- and wakes the owners.  Leadership passes on once
+// the leader's own request is done, so a lone caller sees no queueing delay.
+static void nonce_plus(uint8_t out[24], const uint8_t n0[24], uint64_t x) {
+  memcpy(out, n0, 24);
+  uint64_t carry = 0;
+  for (int i = 0; i < 8; i++) {
+    const uint64_t sum = (uint64_t)out[i] + (uint8_t)(x >> (8 * i)) + carry;
+    out[i] = (uint8_t)sum;
+    carry = sum >> 8;
+  }
+  for (int i = 8; i < 24 && carry; i++) {
+    const uint64_t sum = (uint64_t)out[i] + carry;
+    out[i] = (uint8_t)sum;
+    carry = sum >> 8;
+  }
+}
+
+static NonceArg bounds_arg(uint64_t src_len, uint64_t dst_len);
+
+// Run one combined batch (caller holds e->mu).  Returns XS_OK or an error for all of them.
+static int engine_run_batch(xs_engine* e, std::vector<xs_engine::Req*>& batch) {
+  if (hipSetDevice(e->device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
+  // seal requests first, then open; inside a direction, requests with equal keys adjacent
+  std::stable_sort(batch.begin(), batch.end(), [](const xs_engine::Req* a, const xs_engine::Req* b) {
+    if (a->seal != b->seal) return a->seal;
+    return memcmp(a->key, b->key, 32) < 0;
+  });
+  hipStream_t st = e->slots[0].s;
+  std::vector<uint64_t> blk0(batch.size()), inoff(batch.size()), outoff(batch.size());
+  uint64_t nblk = 0, in_pos = 0, out_pos = 0;
+  for (size_t r = 0; r < batch.size(); r++) {
+    const auto* q = batch[r];
+    blk0[r] = nblk;
+    inoff[r] = in_pos;
+    outoff[r] = out_pos;
+    for (uint64_t j = 0; j < q->nblocks; j++) {
+      xs_block_desc& d = e->h_desc[nblk + j];
+      d.reserved = 0;
+      nonce_plus(d.nonce, q->nonce0, q->first_block + j);
+      if (q->seal) {
+        d.src_off = in_pos + j * XS_BLOCK_DATA;
+        d.dst_off = out_pos + j * XS_BLOCK_SIZE;
+        const uint64_t rem = q->in_len - j * XS_BLOCK_DATA;
+        d.len = (uint32_t)(rem < (uint64_t)XS_BLOCK_DATA ? rem : XS_BLOCK_DATA);
+      } else {
+        d.src_off = in_pos + j * XS_BLOCK_SIZE;
+        d.dst_off = out_pos + j * XS_BLOCK_DATA;
+        const uint64_t rem = q->in_len - j * XS_BLOCK_SIZE;
+        d.len = (uint32_t)(rem < (uint64_t)XS_BLOCK_SIZE ? rem : XS_BLOCK_SIZE) - XS_BLOCK_HDR;
+      }
+    }
+    nblk += q->nblocks;
+    in_pos = (in_pos + q->in_len + 15) & ~15ull;
+    out_pos = (out_pos + q->out_len + 15) & ~15ull;
+  }
+  hipError_t err = hipMemcpyAsync(e->c_desc, e->h_desc, nblk * sizeof(xs_block_desc), hipMemcpyHostToDevice, st);
+  for (size_t r = 0; r < batch.size() && err == hipSuccess; r++)
+    err = hipMemcpyAsync(e->c_in + inoff[r], batch[r]->in, batch[r]->in_len, hipMemcpyHostToDevice, st);
+  if (err != hipSuccess) return hip_fail(err, "coalesced H2D");
+  const NonceArg bounds = bounds_arg(e->c_cap_bytes, e->c_cap_bytes);
+  const xs_block_desc* dd = (const xs_block_desc*)e->c_desc;
+  uint64_t nseal = 0;
+  for (size_t r = 0; r < batch.size();) {  // one keygen per run of (direction, key)
+    size_t r1 = r + 1;
+    while (r1 < batch.size() && batch[r1]->seal == batch[r]->seal && !memcmp(batch[r1]->key, batch[r]->key, 32)) r1++;
+    const uint64_t b0 = blk0[r], b1 = r1 < batch.size() ? blk0[r1] : nblk;
+    err = launch_keygen(batch[r]->seal ? 2 : 3, key_arg(batch[r]->key), bounds, 0, 0, b1 - b0, dd + b0, e->c_keys + b0, st);
+    if (err != hipSuccess) return hip_fail(err, "coalesced keygen");
+    if (batch[r]->seal) nseal = b1;
+    r = r1;
+  }
+  if (nseal) {
+    err = launch_crypt(true, e->c_keys, nseal, e->c_in, e->c_out, nullptr, st);
+    if (err != hipSuccess) return hip_fail(err, "coalesced seal");
+  }
+  if (nblk > nseal) {
+    err = launch_crypt(false, e->c_keys + nseal, nblk - nseal, e->c_in, e->c_out, e->c_ok + nseal, st);
+    if (err != hipSuccess) return hip_fail(err, "coalesced open");
+  }
+  for (size_t r = 0; r < batch.size() && err == hipSuccess; r++) {
+    err = hipMemcpyAsync(batch[r]->out, e->c_out + outoff[r], batch[r]->out_len, hipMemcpyDeviceToHost, st);
+    if (err == hipSuccess && !batch[r]->seal)
+      err = hipMemcpyAsync(batch[r]->ok, e->c_ok + blk0[r], batch[r]->nblocks, hipMemcpyDeviceToHost, st);
+  }
+  if (err != hipSuccess) return hip_fail(err, "coalesced D2H");
+  err = hipStreamSynchronize(st);
+  if (err != hipSuccess) return hip_fail(err, "coalesced stream");
+  return XS_OK;
+}
+
+static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                         const void* in, uint64_t in_len, void* out, uint8_t* ok, uint64_t nblocks) {
+  xs_engine::Req req{};
+  req.seal = seal;
+  memcpy(req.key, key, 32);
+  memcpy(req.nonce0, nonce0, 24);
+  req.first_block = first_block;
+  req.nblocks = nblocks;
+  req.in = (const uint8_t*)in;
+  req.in_len = in_len;
+  req.out = (uint8_t*)out;
+  req.out_len = seal ? in_len + nblocks * XS_BLOCK_HDR : in_len - nblocks * XS_BLOCK_HDR;
+  req.ok = ok;
+  req.rc = XS_OK;
+  req.done = false;
+  std::unique_lock<std::mutex> lk(e->qmu);
+  e->queue.push_back(&req);
+  for (;;) {
+    if (req.done) break;
+    if (!e->leader) {
+      e->leader = true;
+      while (!req.done) {  // lead until our own request is done
+        std::vector<xs_engine::Req*> batch;
+        uint64_t blocks = 0;
+        size_t take = 0;
+        while (take < e->queue.size() && blocks + e->queue[take]->nblocks <= e->c_cap_blocks)
+          blocks += e->queue[take++]->nblocks;
+        batch.assign(e->queue.begin(), e->queue.begin() + take);
+        e->queue.erase(e->queue.begin(), e->queue.begin() + take);
+        lk.unlock();
+        int rc;
+        {
+          std::lock_guard<std::mutex> g(e->mu);
+          rc = engine_run_batch(e, batch);
+        }
+        lk.lock();
+        for (auto* q : batch) {
+          q->rc = rc;
+          q->done = true;
+        }
+        e->st_batches++;
+        e->st_reqs += batch.size();
+        e->st_blocks += blocks;
+      }
+      e->leader = false;
+      e->qcv.notify_all();  // done requests return; a waiting one takes over the lead
+      break;
+    }
+    e->qcv.wait(lk);
+  }
+  return req.rc;
 }
 
 // ---------------------------------------------------------------- seal + MD5 (cryptcheck)

@@ -861,7 +861,6 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
 // (A operand: a Toeplitz window of the wave's LDS table Z, K-group kg <-> row 4u + kg).  Key
 // slots (x = 0, 1) are fed as zero bytes; the key-only terms are in BlockKey::corr.
 typedef int xs_v4i __attribute__((ext_vector_type(4)));
-constexpr int Z_WORDS = 64 * 12;  // 64 rows x 48 bytes
 
 // Column value from its eight 64-bit partial words X[w] (weight 2^(32w), each < 2^50),
 // reduced mod 2^130-5 (limbs < 2^26 + 2^6).

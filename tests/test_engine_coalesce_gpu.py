@@ -1,0 +1,107 @@
+"""Cross-caller coalescing in the host engine (§8(f) rank 2: many concurrent transfers):
+concurrent xs_engine_seal / xs_engine_open calls are packed into combined GPU batches, and
+every caller must get exactly the bytes / ok flags of a separate call -- checked against the
+oracle (cipher.go:737 per block, nonce0 + first_block + i) with two keys, carry-edge nonces,
+first_block offsets, partial last blocks and tampered blocks."""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as orc
+from rclone_amd.testdata import splitmix64_bytes
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from rclone_amd import _lib
+    L = _lib.lib()
+    e = L.xs_engine_create(0, 64, 3)
+    assert e
+    yield L, e
+    L.xs_engine_destroy(e)
+
+
+def _stats(L, e):
+    out = (ctypes.c_uint64 * 3)()
+    L.xs_engine_stats(e, out)
+    return tuple(out)
+
+
+def _seal_expected(plain, nonce0, first, key):
+    out = []
+    for j in range(0, max(1, (len(plain) + 65535) // 65536)):
+        chunk = plain[j * 65536:(j + 1) * 65536]
+        if not chunk:
+            break
+        out.append(orc.seal(chunk, orc.nonce_add(nonce0, first + j), key))
+    return b"".join(out)
+
+
+def _run(L, e, nthreads=12, calls=8):
+    keys = [splitmix64_bytes(1, 32), splitmix64_bytes(2, 32)]
+    errors = []
+    start = threading.Barrier(nthreads)
+
+    def worker(t):
+        try:
+            start.wait()
+            for i in range(calls):
+                key = keys[(t + i) % 2]
+                n = [1, 100, 65536, 65537, 3 * 65536 - 5, 200000][(t * 3 + i) % 6]
+                plain = splitmix64_bytes(1000 * t + i, n)
+                nonce0 = b"\xfe" + b"\xff" * 7 + splitmix64_bytes(t, 16) if i % 3 == 0 else splitmix64_bytes(7 * t + i, 24)
+                first = [0, 1, 255, 1 << 33][i % 4]
+                nb = (n + 65535) // 65536
+                body = ctypes.create_string_buffer(n + 16 * nb)
+                assert L.xs_engine_seal(e, key, nonce0, first, plain, n, body) == 0
+                want = _seal_expected(plain, nonce0, first, key)
+                assert body.raw == want, (t, i, n)
+                wire = bytearray(want)
+                bad = set()
+                if i % 2 and nb > 1:
+                    wire[65552 + 5] ^= 1  # a tag byte of block 1
+                    bad.add(1)
+                out = ctypes.create_string_buffer(n)
+                ok = (ctypes.c_uint8 * nb)()
+                assert L.xs_engine_open(e, key, nonce0, first, bytes(wire), len(wire), out, ok) == 0
+                assert [j for j in range(nb) if not ok[j]] == sorted(bad), (t, i)
+                exp = bytearray(plain)
+                for j in bad:
+                    exp[j * 65536:(j + 1) * 65536] = bytes(len(exp[j * 65536:(j + 1) * 65536]))
+                assert out.raw == bytes(exp), (t, i)
+        except BaseException as ex:  # noqa: BLE001
+            errors.append((t, repr(ex)))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[:3]
+    return nthreads * calls * 2
+
+
+def test_coalesced_engine_matches_oracle(eng):
+    L, e = eng
+    L.xs_engine_set_coalesce(e, 1)
+    b0, r0, k0 = _stats(L, e)
+    ncalls = _run(L, e)
+    b1, r1, k1 = _stats(L, e)
+    assert r1 - r0 == ncalls               # every call went through the coalescer
+    assert b1 - b0 < r1 - r0               # and some of them shared a GPU batch
+
+
+def test_uncoalesced_engine_matches_oracle(eng):
+    L, e = eng
+    L.xs_engine_set_coalesce(e, 0)
+    before = _stats(L, e)
+    _run(L, e, nthreads=4, calls=6)
+    assert _stats(L, e) == before
+    L.xs_engine_set_coalesce(e, 1)
