@@ -287,9 +287,17 @@ struct xs_engine {
   std::condition_variable qcv;
   std::vector<Req*> queue;
   bool leader = false;
-  uint8_t *c_in = nullptr, *c_out = nullptr, *c_ok = nullptr, *c_desc = nullptr;
-  BlockKey* c_keys = nullptr;
-  xs_block_desc* h_desc = nullptr;  // pinned
+  struct CSlot {  // one combined batch in flight
+    hipStream_t s = nullptr;
+    hipEvent_t done = nullptr;
+    uint8_t *in = nullptr, *out = nullptr, *ok = nullptr, *desc = nullptr;
+    BlockKey* keys = nullptr;
+    xs_block_desc* h_desc = nullptr;  // pinned
+    std::vector<Req*> batch;
+    uint64_t blocks = 0;
+    int rc = XS_OK;
+  };
+  std::vector<CSlot> cslots;
   uint64_t c_cap_blocks = 0, c_cap_bytes = 0;
   uint64_t st_batches = 0, st_reqs = 0, st_blocks = 0;
   // grow-only buffers of xs_engine_seal_md5 (whole objects per group)
@@ -325,12 +333,17 @@ static void engine_free(xs_engine* e) {
     (void)hipFree(sl.d_ok);
     if (sl.s) (void)hipStreamDestroy(sl.s);
   }
-  (void)hipFree(e->c_in);
-  (void)hipFree(e->c_out);
-  (void)hipFree(e->c_ok);
-  (void)hipFree(e->c_desc);
-  (void)hipFree(e->c_keys);
-  (void)hipHostFree(e->h_desc);
+  for (auto& c : e->cslots) {
+    if (c.s) (void)hipStreamSynchronize(c.s);
+    (void)hipFree(c.in);
+    (void)hipFree(c.out);
+    (void)hipFree(c.ok);
+    (void)hipFree(c.desc);
+    (void)hipFree(c.keys);
+    (void)hipHostFree(c.h_desc);
+    if (c.done) (void)hipEventDestroy(c.done);
+    if (c.s) (void)hipStreamDestroy(c.s);
+  }
   (void)hipFree(e->hb.d_plain);
   (void)hipFree(e->hb.d_body);
   (void)hipFree(e->hb.d_desc);
@@ -371,14 +384,19 @@ extern "C" xs_engine* xs_engine_create(int device, uint32_t batch_blocks, int ns
   // (+16 bytes of alignment slack per block for the per-request 16-byte alignment)
   e->c_cap_blocks = batch_blocks;
   e->c_cap_bytes = (uint64_t)batch_blocks * (XS_BLOCK_SIZE + 16);
-  if (hipMalloc(&e->c_in, e->c_cap_bytes) != hipSuccess || hipMalloc(&e->c_out, e->c_cap_bytes) != hipSuccess ||
-      hipMalloc(&e->c_ok, batch_blocks) != hipSuccess ||
-      hipMalloc(&e->c_desc, (size_t)batch_blocks * sizeof(xs_block_desc)) != hipSuccess ||
-      hipMalloc(&e->c_keys, (size_t)batch_blocks * sizeof(BlockKey)) != hipSuccess ||
-      hipHostMalloc(&e->h_desc, (size_t)batch_blocks * sizeof(xs_block_desc), hipHostMallocPortable) != hipSuccess) {
-    set_error("xs_engine_create: device allocation failed");
-    engine_free(e);
-    return nullptr;
+  e->cslots.resize(nslots);
+  for (auto& c : e->cslots) {
+    if (hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c.done, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc(&c.in, e->c_cap_bytes) != hipSuccess || hipMalloc(&c.out, e->c_cap_bytes) != hipSuccess ||
+        hipMalloc(&c.ok, batch_blocks) != hipSuccess ||
+        hipMalloc(&c.desc, (size_t)batch_blocks * sizeof(xs_block_desc)) != hipSuccess ||
+        hipMalloc(&c.keys, (size_t)batch_blocks * sizeof(BlockKey)) != hipSuccess ||
+        hipHostMalloc(&c.h_desc, (size_t)batch_blocks * sizeof(xs_block_desc), hipHostMallocPortable) != hipSuccess) {
+      set_error("xs_engine_create: device allocation failed");
+      engine_free(e);
+      return nullptr;
+    }
   }
   if (const char* v = getenv("XS_ENGINE_COALESCE")) e->coalesce = atoi(v) != 0;
   return e;
@@ -522,15 +540,16 @@ static void nonce_plus(uint8_t out[24], const uint8_t n0[24], uint64_t x) {
 
 static NonceArg bounds_arg(uint64_t src_len, uint64_t dst_len);
 
-// Run one combined batch (caller holds e->mu).  Returns XS_OK or an error for all of them.
-static int engine_run_batch(xs_engine* e, std::vector<xs_engine::Req*>& batch) {
+// Issue one combined batch on coalescing slot c (asynchronously; completion = c.done).
+static int engine_issue_batch(xs_engine* e, xs_engine::CSlot& c) {
+  auto& batch = c.batch;
   if (hipSetDevice(e->device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
   // seal requests first, then open; inside a direction, requests with equal keys adjacent
   std::stable_sort(batch.begin(), batch.end(), [](const xs_engine::Req* a, const xs_engine::Req* b) {
     if (a->seal != b->seal) return a->seal;
     return memcmp(a->key, b->key, 32) < 0;
   });
-  hipStream_t st = e->slots[0].s;
+  hipStream_t st = c.s;
   std::vector<uint64_t> blk0(batch.size()), inoff(batch.size()), outoff(batch.size());
   uint64_t nblk = 0, in_pos = 0, out_pos = 0;
   for (size_t r = 0; r < batch.size(); r++) {
@@ -539,7 +558,7 @@ static int engine_run_batch(xs_engine* e, std::vector<xs_engine::Req*>& batch) {
     inoff[r] = in_pos;
     outoff[r] = out_pos;
     for (uint64_t j = 0; j < q->nblocks; j++) {
-      xs_block_desc& d = e->h_desc[nblk + j];
+      xs_block_desc& d = c.h_desc[nblk + j];
       d.reserved = 0;
       nonce_plus(d.nonce, q->nonce0, q->first_block + j);
       if (q->seal) {
@@ -558,38 +577,37 @@ static int engine_run_batch(xs_engine* e, std::vector<xs_engine::Req*>& batch) {
     in_pos = (in_pos + q->in_len + 15) & ~15ull;
     out_pos = (out_pos + q->out_len + 15) & ~15ull;
   }
-  hipError_t err = hipMemcpyAsync(e->c_desc, e->h_desc, nblk * sizeof(xs_block_desc), hipMemcpyHostToDevice, st);
+  hipError_t err = hipMemcpyAsync(c.desc, c.h_desc, nblk * sizeof(xs_block_desc), hipMemcpyHostToDevice, st);
   for (size_t r = 0; r < batch.size() && err == hipSuccess; r++)
-    err = hipMemcpyAsync(e->c_in + inoff[r], batch[r]->in, batch[r]->in_len, hipMemcpyHostToDevice, st);
+    err = hipMemcpyAsync(c.in + inoff[r], batch[r]->in, batch[r]->in_len, hipMemcpyHostToDevice, st);
   if (err != hipSuccess) return hip_fail(err, "coalesced H2D");
   const NonceArg bounds = bounds_arg(e->c_cap_bytes, e->c_cap_bytes);
-  const xs_block_desc* dd = (const xs_block_desc*)e->c_desc;
+  const xs_block_desc* dd = (const xs_block_desc*)c.desc;
   uint64_t nseal = 0;
   for (size_t r = 0; r < batch.size();) {  // one keygen per run of (direction, key)
     size_t r1 = r + 1;
     while (r1 < batch.size() && batch[r1]->seal == batch[r]->seal && !memcmp(batch[r1]->key, batch[r]->key, 32)) r1++;
     const uint64_t b0 = blk0[r], b1 = r1 < batch.size() ? blk0[r1] : nblk;
-    err = launch_keygen(batch[r]->seal ? 2 : 3, key_arg(batch[r]->key), bounds, 0, 0, b1 - b0, dd + b0, e->c_keys + b0, st);
+    err = launch_keygen(batch[r]->seal ? 2 : 3, key_arg(batch[r]->key), bounds, 0, 0, b1 - b0, dd + b0, c.keys + b0, st);
     if (err != hipSuccess) return hip_fail(err, "coalesced keygen");
     if (batch[r]->seal) nseal = b1;
     r = r1;
   }
   if (nseal) {
-    err = launch_crypt(true, e->c_keys, nseal, e->c_in, e->c_out, nullptr, st);
+    err = launch_crypt(true, c.keys, nseal, c.in, c.out, nullptr, st);
     if (err != hipSuccess) return hip_fail(err, "coalesced seal");
   }
   if (nblk > nseal) {
-    err = launch_crypt(false, e->c_keys + nseal, nblk - nseal, e->c_in, e->c_out, e->c_ok + nseal, st);
+    err = launch_crypt(false, c.keys + nseal, nblk - nseal, c.in, c.out, c.ok + nseal, st);
     if (err != hipSuccess) return hip_fail(err, "coalesced open");
   }
   for (size_t r = 0; r < batch.size() && err == hipSuccess; r++) {
-    err = hipMemcpyAsync(batch[r]->out, e->c_out + outoff[r], batch[r]->out_len, hipMemcpyDeviceToHost, st);
+    err = hipMemcpyAsync(batch[r]->out, c.out + outoff[r], batch[r]->out_len, hipMemcpyDeviceToHost, st);
     if (err == hipSuccess && !batch[r]->seal)
-      err = hipMemcpyAsync(batch[r]->ok, e->c_ok + blk0[r], batch[r]->nblocks, hipMemcpyDeviceToHost, st);
+      err = hipMemcpyAsync(batch[r]->ok, c.ok + blk0[r], batch[r]->nblocks, hipMemcpyDeviceToHost, st);
   }
+  if (err == hipSuccess) err = hipEventRecord(c.done, st);
   if (err != hipSuccess) return hip_fail(err, "coalesced D2H");
-  err = hipStreamSynchronize(st);
-  if (err != hipSuccess) return hip_fail(err, "coalesced stream");
   return XS_OK;
 }
 
@@ -610,38 +628,56 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
   req.done = false;
   std::unique_lock<std::mutex> lk(e->qmu);
   e->queue.push_back(&req);
-  for (;;) {
-    if (req.done) break;
-    if (!e->leader) {
-      e->leader = true;
-      while (!req.done) {  // lead until our own request is done
-        std::vector<xs_engine::Req*> batch;
-        uint64_t blocks = 0;
+  while (!req.done) {
+    if (e->leader) {
+      e->qcv.wait(lk);
+      continue;
+    }
+    // lead: keep up to nslots combined batches in flight until our own request is done and
+    // nothing is in flight, then hand over
+    e->leader = true;
+    const size_t ns = e->cslots.size();
+    size_t head = 0, inflight = 0;  // ring of slots: [head, head + inflight) are in flight
+    while (!(req.done && inflight == 0)) {
+      if (inflight < ns && !e->queue.empty() && !req.done) {
+        auto& c = e->cslots[(head + inflight) % ns];
+        c.batch.clear();
+        c.blocks = 0;
         size_t take = 0;
-        while (take < e->queue.size() && blocks + e->queue[take]->nblocks <= e->c_cap_blocks)
-          blocks += e->queue[take++]->nblocks;
-        batch.assign(e->queue.begin(), e->queue.begin() + take);
+        while (take < e->queue.size() && c.blocks + e->queue[take]->nblocks <= e->c_cap_blocks)
+          c.blocks += e->queue[take++]->nblocks;
+        c.batch.assign(e->queue.begin(), e->queue.begin() + take);
         e->queue.erase(e->queue.begin(), e->queue.begin() + take);
         lk.unlock();
-        int rc;
-        {
-          std::lock_guard<std::mutex> g(e->mu);
-          rc = engine_run_batch(e, batch);
-        }
+        c.rc = engine_issue_batch(e, c);
         lk.lock();
-        for (auto* q : batch) {
-          q->rc = rc;
-          q->done = true;
-        }
-        e->st_batches++;
-        e->st_reqs += batch.size();
-        e->st_blocks += blocks;
+        inflight++;
+        continue;
       }
-      e->leader = false;
-      e->qcv.notify_all();  // done requests return; a waiting one takes over the lead
-      break;
+      if (inflight == 0) break;  // nothing queued for us (own request already done)
+      auto& c = e->cslots[head];
+      lk.unlock();
+      if (c.rc == XS_OK) {
+        hipError_t err = hipEventSynchronize(c.done);
+        if (err != hipSuccess) c.rc = hip_fail(err, "coalesced stream");
+      } else {
+        (void)hipStreamSynchronize(c.s);
+      }
+      lk.lock();
+      for (auto* q : c.batch) {
+        q->rc = c.rc;
+        q->done = true;
+      }
+      e->st_batches++;
+      e->st_reqs += c.batch.size();
+      e->st_blocks += c.blocks;
+      c.batch.clear();
+      head = (head + 1) % ns;
+      inflight--;
+      e->qcv.notify_all();
     }
-    e->qcv.wait(lk);
+    e->leader = false;
+    e->qcv.notify_all();  // a waiting caller with a queued request takes over the lead
   }
   return req.rc;
 }
