@@ -14,7 +14,9 @@ struct NonceArg {
   uint32_t n[6];
 };
 
-// Per-block key schedule written by xs_keygen, read by xs_crypt (2272 bytes).
+// Per-block key schedule written by xs_keygen, read by xs_seal / xs_open (976 bytes).  Power
+// tables (radix-2^26 limbs, uncanonicalised pmul outputs) depend on the block's length:
+// full 64 KiB blocks take the matrix-core path, shorter ones the VALU Horner path.
 struct __attribute__((aligned(16))) BlockKey {
   uint32_t subkey[8];  // HSalsa20(key, nonce[0:16])
   uint32_t n2[2];      // nonce[16:24] (Salsa20 words 6, 7)
@@ -25,16 +27,23 @@ struct __attribute__((aligned(16))) BlockKey {
   uint32_t s[4];       // Poly1305 s
   uint32_t ks1024[8];  // keystream block 1024 words 0..7 (message chunks 4094, 4095)
   uint32_t r[5];       // clamped r, radix 2^26
-  uint32_t R[5];       // r^253 (gap between a lane's chunk groups)
-  uint32_t pad[2];
-  uint32_t T1[32][5];  // r^0 .. r^31
-  uint32_t T2[8][5];   // r^(32a), a = 0..7 (a lane's final exponent is < 256)
-  // matrix-core Poly1305 (full blocks only, xs_kernels.hip crypt_block_mfma)
-  uint32_t W[64][5];   // r^(64k), k = 0..63: weight of 64-chunk group g is W[63-g]
-  uint32_t corr[5];    // key-only correction term added once per block
-  uint32_t pad2[3];
+  uint32_t R[5];       // partial blocks: r^253 (gap between a lane's chunk groups)
+  uint32_t corr[5];    // full blocks: key-only correction term added once per block
+  uint32_t pad[1];
+  union {
+    struct {             // partial blocks (crypt_block)
+      uint32_t T1[32][5];  // r^0 .. r^31
+      uint32_t T2[8][5];   // r^(32a), a = 0..7 (a lane's final exponent is < 256)
+    } part;
+    struct {             // full blocks (crypt_block_mfma): r^(64k) = A[k&7] B[k>>3], r^e = C[e&7] D[e>>3]
+      uint32_t A[8][5];    // r^(64i)
+      uint32_t B[8][5];    // r^(512j)
+      uint32_t C[8][5];    // r^b
+      uint32_t D[9][5];    // r^(8a), a = 0..8
+    } full;
+  };
 };
-static_assert(sizeof(BlockKey) == 2272, "BlockKey layout");
+static_assert(sizeof(BlockKey) == 976, "BlockKey layout");
 
 hipError_t launch_keygen(int mode, const KeyArg& key, const NonceArg& nonce0, uint64_t first_block,
                          uint64_t total_len, uint64_t nblocks, const xs_block_desc* desc, BlockKey* out,

@@ -431,36 +431,83 @@ __device__ __forceinline__ P5 psub(const P5& a, const P5& b) {
   return o;
 }
 
-__device__ void mfma_tables(const P5& r, const P5& r32, BlockKey* __restrict__ o) {
-  // S = sum_{e=3..66} r^e, and r^65, r^66
-  P5 pw = pcanon(pmul(pmul(r, r), r));  // r^3
-  P5 S = pw, r65 = pw, r66 = pw;
-  for (int e = 4; e <= 66; e++) {
-    pw = pcanon(pmul(pw, r));
+// radix-2^26 limbs of a 16-byte little-endian chunk without the pad bit
+__device__ __forceinline__ P5 chunk26(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  P5 o;
+  o.v[0] = w0 & M26;
+  o.v[1] = alignbit(w1, w0, 26) & M26;
+  o.v[2] = alignbit(w2, w1, 20) & M26;
+  o.v[3] = alignbit(w3, w2, 14) & M26;
+  o.v[4] = w3 >> 8;
+  return o;
+}
+
+// Full-block tables and correction.  The Toeplitz weights W_k = r^(64k) (k = 0..63) are
+// A[k&7] B[k>>3] and the column exponents r^e (e = 3..66) are C[e&7] D[e>>3]; the kernel forms
+// the one product each lane needs.  S = sum_{e=3..66} r^e = r^3 (1 + r^32) (sum C)(D0+..+D3),
+// sum_k W_k = (sum A)(sum B).  SEAL: the key slots hash the keystream words that the
+// kernel's zeroed staging slot XORs into them (chunk -2 = ks[0..3] at exponent 4098, chunk -1 =
+// ks[4..7] at 4097), so corr also removes W_63 (ks_lo r^66 + ks_hi r^65); OPEN hashes zero
+// bytes there (the staged wire data of those slots is zero).
+__device__ __forceinline__ void put5(uint32_t (&dst)[5], const P5& v) {
 #pragma unroll
-    for (int i = 0; i < 5; i++) S.v[i] += pw.v[i];
-    if (e == 65) r65 = pw;
-    if (e == 66) r66 = pw;
-    if ((e & 7) == 0) S = pcanon(S);
+  for (int i = 0; i < 5; i++) dst[i] = v.v[i];
+}
+
+__device__ __forceinline__ void add5(P5& a, const P5& b) {
+#pragma unroll
+  for (int i = 0; i < 5; i++) a.v[i] += b.v[i];
+}
+
+__device__ void full_tables(bool seal, const P5& r, const uint32_t (&ks)[16], BlockKey* __restrict__ o) {
+  P5 one;
+  one.v[0] = 1; one.v[1] = one.v[2] = one.v[3] = one.v[4] = 0;
+  // C_b = r^b
+  P5 p = one, sumC = one;
+  put5(o->full.C[0], one);
+  for (int b = 1; b < 8; b++) {
+    p = pmul(p, r);
+    put5(o->full.C[b], p);
+    add5(sumC, p);
   }
-  S = pcanon(S);
-  // W_k = r^(64k), sum_k W_k
-  const P5 r64 = pcanon(pmul(r32, r32));
-  P5 w, SW;
-  w.v[0] = 1; w.v[1] = w.v[2] = w.v[3] = w.v[4] = 0;
-  SW = w;
-#pragma unroll
-  for (int i = 0; i < 5; i++) o->W[0][i] = w.v[i];
-  for (int k = 1; k < 64; k++) {
-    w = pcanon(pmul(w, r64));
-#pragma unroll
-    for (int i = 0; i < 5; i++) {
-      o->W[k][i] = w.v[i];
-      SW.v[i] += w.v[i];
-    }
-    if ((k & 7) == 0) SW = pcanon(SW);
+  const P5 r3 = pmul(pmul(r, r), r);
+  const P5 r8 = pmul(p, r);
+  // D_a = r^(8a), a = 0..8
+  P5 q = one, sumD4 = one, r32 = one;
+  put5(o->full.D[0], one);
+  for (int a = 1; a <= 8; a++) {
+    q = pmul(q, r8);
+    put5(o->full.D[a], q);
+    if (a < 4) add5(sumD4, q);
+    if (a == 4) r32 = q;
   }
-  SW = pcanon(SW);  // w = W_63 now
+  const P5 r64 = q;
+  // A_i = r^(64i), B_j = r^(512j)
+  P5 w = one, sumA = one;
+  put5(o->full.A[0], one);
+  for (int i = 1; i < 8; i++) {
+    w = pmul(w, r64);
+    put5(o->full.A[i], w);
+    add5(sumA, w);
+  }
+  const P5 r512 = pmul(w, r64);
+  P5 v = one, sumB = one;
+  put5(o->full.B[0], one);
+  for (int j = 1; j < 8; j++) {
+    v = pmul(v, r512);
+    put5(o->full.B[j], v);
+    add5(sumB, v);
+  }
+  const P5 W63 = pmul(w, v);
+  pnorm(sumA);
+  pnorm(sumB);
+  const P5 SW = pcanon(pmul(sumA, sumB));
+  pnorm(sumC);
+  pnorm(sumD4);
+  P5 one_r32 = r32;
+  one_r32.v[0] += 1;
+  const P5 S = pcanon(pmul(pmul(pmul(r3, sumC), sumD4), one_r32));
+  const P5 r65 = pmul(r64, r), r66 = pmul(r65, r);
   P5 E, B, two128;
 #pragma unroll
   for (int i = 0; i < 5; i++) {
@@ -472,12 +519,17 @@ __device__ void mfma_tables(const P5& r, const P5& r32, BlockKey* __restrict__ o
   const P5 es_b = pcanon(psub(pcanon(pmul(E, SW)), B));
   const P5 a = pcanon(pmul(S, es_b));
   P5 kk = r65;
-#pragma unroll
-  for (int i = 0; i < 5; i++) kk.v[i] += r66.v[i];
-  const P5 b = pcanon(pmul(pmul(two128, pcanon(kk)), w));
+  add5(kk, r66);
+  pnorm(kk);
+  kk = pmul(two128, kk);
+  if (seal) {  // + ks_lo r^66 + ks_hi r^65 (the key-slot bytes; their pad bits are the 2^128 term)
+    add5(kk, pmul(chunk26(ks[0], ks[1], ks[2], ks[3]), r66));
+    add5(kk, pmul(chunk26(ks[4], ks[5], ks[6], ks[7]), r65));
+    pnorm(kk);
+  }
+  const P5 b = pcanon(pmul(kk, W63));
   const P5 c = pcanon(psub(a, b));
-#pragma unroll
-  for (int i = 0; i < 5; i++) o->corr[i] = c.v[i];
+  put5(o->corr, c);
 }
 
 // ---------------------------------------------------------------- keygen
@@ -578,32 +630,31 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
   }
 #pragma unroll
   for (int i = 0; i < 5; i++) o->r[i] = r.v[i];
-  P5 p;
-  p.v[0] = 1; p.v[1] = 0; p.v[2] = 0; p.v[3] = 0; p.v[4] = 0;
-  for (int i = 0; i < 32; i++) {
-#pragma unroll
-    for (int j = 0; j < 5; j++) o->T1[i][j] = p.v[j];
-    if (i < 31) p = pcanon(pmul(p, r));
+  if (len == XS_BLOCK_DATA) {
+    full_tables(MODE == 0 || MODE == 2, r, ks, o);
+    return;
   }
-  P5 r32 = pcanon(pmul(p, r));
+  // partial block: power tables for the VALU Horner.  pmul outputs (limbs < 2^26, limb 1 <
+  // 2^26 + 2^6) are valid multipliers, so the chains stay uncanonicalised.
+  P5 p, r29;
   p.v[0] = 1; p.v[1] = 0; p.v[2] = 0; p.v[3] = 0; p.v[4] = 0;
+  r29 = p;
+  for (int i = 0; i < 32; i++) {
+    put5(o->part.T1[i], p);
+    if (i == 29) r29 = p;
+    if (i < 31) p = pmul(p, r);
+  }
+  const P5 r32 = pmul(p, r);
+  p.v[0] = 1; p.v[1] = 0; p.v[2] = 0; p.v[3] = 0; p.v[4] = 0;
+  P5 r224 = p;
   for (int a = 0; a < 8; a++) {
-#pragma unroll
-    for (int j = 0; j < 5; j++) o->T2[a][j] = p.v[j];
-    if (a < 7) p = pcanon(pmul(p, r32));
+    put5(o->part.T2[a], p);
+    if (a == 7) r224 = p;
+    if (a < 7) p = pmul(p, r32);
   }
   // r^253 = r^224 * r^29: the Horner gap between a lane's consecutive chunk groups
   // (64 lanes per block, 4 chunks per group: 4*64 - 3)
-  P5 r29, r224;
-#pragma unroll
-  for (int j = 0; j < 5; j++) {
-    r29.v[j] = o->T1[29][j];
-    r224.v[j] = o->T2[7][j];
-  }
-  P5 R = pcanon(pmul(r224, r29));
-#pragma unroll
-  for (int i = 0; i < 5; i++) o->R[i] = R.v[i];
-  if (len == XS_BLOCK_DATA) mfma_tables(r, r32, o);
+  put5(o->R, pmul(r224, r29));
 }
 
 // ---------------------------------------------------------------- main block kernel
@@ -619,7 +670,10 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
 // 1024, precomputed by keygen), so every lane's Horner multipliers are uniform: r inside a
 // group, r^253 between groups.
 #ifndef XS_POLY_MFMA
-#define XS_POLY_MFMA 1  // full-block Poly1305 on the matrix cores (0: radix-2^32 VALU Horner)
+#define XS_POLY_MFMA 1  // full-block Poly1305 on the matrix cores
+#endif
+#if !XS_POLY_MFMA
+#error "full blocks need the matrix-core path: keygen writes no T1/T2 tables for them"
 #endif
 #if XS_POLY_MFMA
 constexpr int WAVE_LDS_WORDS = 1024 + 768;  // 4 KiB staging + 3 KiB Toeplitz table
@@ -679,8 +733,8 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
       const uint32_t e = (l == 63u) ? 0u : 254u - 4u * l;
 #pragma unroll
       for (int i = 0; i < 5; i++) {
-        t1.v[i] = bk->T1[e & 31u][i];
-        t2.v[i] = bk->T2[e >> 5][i];
+        t1.v[i] = bk->part.T1[e & 31u][i];
+        t2.v[i] = bk->part.T2[e >> 5][i];
       }
     }
     uint32_t ks[16];
@@ -837,8 +891,8 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
       const uint32_t e = (uint32_t)(nc - 1 - c_last);
 #pragma unroll
       for (int i = 0; i < 5; i++) {
-        t1.v[i] = bk->T1[e & 31u][i];
-        t2.v[i] = bk->T2[e >> 5][i];
+        t1.v[i] = bk->part.T1[e & 31u][i];
+        t2.v[i] = bk->part.T2[e >> 5][i];
       }
       h = pmul(h, pmul(t1, t2));
     }
@@ -899,13 +953,18 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
                                                  uint8_t* __restrict__ pout, uint32_t* wb, uint32_t* zb, P5& h) {
   const uint32_t l = threadIdx.x & 63u, n = l & 15u, kg = l >> 4;
   // ---- Z table: row p = l holds the signed digits D_0..D_16 of r^(64(63-p)) reversed,
-  // Z[u] = D_{31-u} for 15 <= u <= 31, zero elsewhere (12 words per row).
+  // Z[u] = D_{31-u} for 15 <= u <= 31, zero elsewhere (12 words per row).  W is stored
+  // uncanonicalised (< 2^131): repack the limbs with carries, any representative works.
   {
-    uint32_t q[5];
+    P5 qa, qb;
+    const uint32_t k = 63u - l;
 #pragma unroll
-    for (int i = 0; i < 5; i++) q[i] = bk->W[63u - l][i];  // canonical
-    uint32_t w0 = q[0] | (q[1] << 26), w1 = (q[1] >> 6) | (q[2] << 20), w2 = (q[2] >> 12) | (q[3] << 14),
-             w3 = (q[3] >> 18) | (q[4] << 8), w4 = q[4] >> 24;
+    for (int i = 0; i < 5; i++) {
+      qa.v[i] = bk->full.A[k & 7u][i];
+      qb.v[i] = bk->full.B[k >> 3][i];
+    }
+    const P32 wq = to32(pmul(qa, qb));
+    uint32_t w0 = wq.w0, w1 = wq.w1, w2 = wq.w2, w3 = wq.w3, w4 = wq.w4;
     unsigned cy;  // +0x80 in every byte, carried; flipping each byte's top bit then gives digits in [-128, 127]
     w0 = __builtin_addc(w0, 0x80808080u, 0u, &cy);
     w1 = __builtin_addc(w1, 0x80808080u, cy, &cy);
@@ -921,6 +980,12 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
     row[1] = make_uint4(__builtin_bswap32(w3), __builtin_bswap32(w2), __builtin_bswap32(w1), __builtin_bswap32(w0));
     row[2] = make_uint4(0u, 0u, 0u, 0u);
   }
+  // key slots (chunks -2, -1 = lane 0's first two staging chunks of super-iteration 0) are never
+  // loaded: zero them, so OPEN hashes zero bytes there and SEAL the keystream (keygen's corr)
+  if (l == 0u) {
+    *reinterpret_cast<uint4*>(wb) = make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>(wb + 256) = make_uint4(0u, 0u, 0u, 0u);
+  }
   uint32_t k[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) k[i] = bk->subkey[i];
@@ -928,6 +993,8 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
   // A window for output q = 16mt + n starts at Z byte 31 - q: words zlo .. zlo + 8 cover both
   // halves (mt = 1 at word zlo, mt = 0 at word zlo + 4), byte shift zsh
   const uint32_t zlo = (15u - n) >> 2, zsh = (31u - n) & 3u;
+  const uint8_t* pin_m32 = pin - 32;
+  uint8_t* pout_m32 = pout - 32;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own Z writes are visible
   xs_v4i acc[4][2];
 #pragma unroll
@@ -940,10 +1007,11 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
   for (int u = 0; u < 16; u++) {
     const uint32_t K = 64u * u + l;
     const bool key_slots = K == 0u;  // chunks -2, -1: the Poly1305 key, not message
-    const uint8_t* src = pin + 64u * K - 32u;
+    const uint32_t off = 64u * K;    // byte offset from pin - 32 (uniform base, 32-bit offset)
 #pragma unroll
     for (int j = 0; j < 4; j++)
-      if (j >= 2 || !key_slots) __builtin_amdgcn_global_load_lds(src + 16 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
+      if (j >= 2 || !key_slots)
+        __builtin_amdgcn_global_load_lds(pin_m32 + off + 16 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
     uint32_t ks[16];
     salsa20_block_pre(pre, K, ks);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -956,11 +1024,10 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
     uint32_t o[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) o[i] = d[i] ^ ks[i];
-    uint8_t* dst = pout + 64u * K - 32u;
 #pragma unroll
     for (int j = 0; j < 4; j++)
       if (j >= 2 || !key_slots)
-        *reinterpret_cast<uint4*>(dst + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
+        *reinterpret_cast<uint4*>(pout_m32 + off + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
     // A operands of row 4u + kg for both output halves
     const uint32_t* zr = zb + 12u * (4u * u + kg) + zlo;
     uint32_t z[9];
@@ -975,10 +1042,9 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
     const uint32_t* cw = SEAL ? o : d;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const bool zero = key_slots && j < 2;
       xs_v4i B;
 #pragma unroll
-      for (int i = 0; i < 4; i++) B[i] = (int)(zero ? 0x80808080u : (cw[4 * j + i] ^ 0x80808080u));
+      for (int i = 0; i < 4; i++) B[i] = (int)(cw[4 * j + i] ^ 0x80808080u);
 #pragma unroll
       for (int mt = 0; mt < 2; mt++) acc[j][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[mt], B, acc[j][mt], 0, 0, 0);
     }
@@ -1013,10 +1079,10 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
     P5 t1, t2;
 #pragma unroll
     for (int i = 0; i < 5; i++) {
-      t1.v[i] = bk->T1[e & 31u][i];
-      t2.v[i] = bk->T2[e >> 5][i];
+      t1.v[i] = bk->full.C[e & 7u][i];
+      t2.v[i] = bk->full.D[e >> 3][i];
     }
-    hs = pmul(V, pcanon(pmul(t2, t1)));
+    hs = pmul(V, pmul(t2, t1));
   }
   if (l == 0u) {
 #pragma unroll
@@ -1054,7 +1120,7 @@ template <bool SEAL>
 __device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, uint64_t nblocks,
                                            const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                            uint8_t* __restrict__ ok, uint32_t* lds) {
-  const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63u;
   // wave-uniform block index
   const uint64_t blk = (uint64_t)blockIdx.x * 4u + (uint64_t)__builtin_amdgcn_readfirstlane(wave);
   if (blk >= nblocks) return;

@@ -1,12 +1,23 @@
 #!/bin/bash
-# Build tools/abtest_<name>: A = current xs_kernels.hip defaults, B = same source with the
-# given -D macros.   usage: tools/abtest.sh <name> [-DMACRO=...]...
+# Build tools/abtest_<name>: A = xs_kernels.hip at git revision $AREF (default HEAD) or, with
+# AREF=tree, the working tree; B = the working tree's xs_kernels.hip with the given -D macros.
+#   usage: [AREF=<rev>|tree] tools/abtest.sh <name> [-DMACRO=...]...
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
 D=/tmp/abtest
 mkdir -p $D
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c rclone_amd/csrc/xs_kernels.hip -I rclone_amd/csrc -o $D/a.o
+AREF=${AREF:-HEAD}
+if [ "$AREF" = tree ]; then
+  cp rclone_amd/csrc/xs_kernels.hip $D/a_src.hip
+  cp rclone_amd/csrc/xs_internal.h $D/
+else
+  git show "$AREF":rclone_amd/csrc/xs_kernels.hip > $D/a_src.hip
+  git show "$AREF":rclone_amd/csrc/xs_internal.h > $D/xs_internal.h
+fi
+mkdir -p $D/include && cp include/rclone_crypt_gpu.h $D/include/
+sed -i 's#"../../include/rclone_crypt_gpu.h"#"include/rclone_crypt_gpu.h"#' $D/xs_internal.h
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c $D/a_src.hip -I $D -o $D/a.o
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c rclone_amd/csrc/xs_kernels.hip -I rclone_amd/csrc -Dxs=xs_b "$@" -o $D/b_$name.o
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -c tools/abtest.cpp -I rclone_amd/csrc -o $D/t.o
 hipcc --offload-arch=gfx950 $D/t.o $D/a.o $D/b_$name.o -o tools/abtest_$name
