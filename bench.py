@@ -42,8 +42,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10, help="untimed steps; the clock settles over the first ~6")
     ap.add_argument("--blocks", type=int, default=100_000, help="64 KiB blocks per GPU")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -285,6 +285,9 @@ def main():
     el = float(tmax.item())
     seal_ms = [a.elapsed_time(b) for s, a, b in ev if s]
     open_ms = [a.elapsed_time(b) for s, a, b in ev if not s]
+    if os.environ.get("BENCH_TRACE"):
+        print("seal_ms", [round(x, 3) for x in seal_ms], "\nopen_ms", [round(x, 3) for x in open_ms],
+              file=sys.stderr)
     seal_avg = sum(seal_ms) / len(seal_ms)
     open_avg = sum(open_ms) / len(open_ms)
     total_bytes = int(counters[1].item())

@@ -31,6 +31,9 @@
 
 // XS_SEAL_WPE / XS_OPEN_WPE: minimum waves per SIMD the register allocator must allow
 // (amdgpu_waves_per_eu) for the seal / open kernels.
+#ifndef XS_XCD_REMAP
+#define XS_XCD_REMAP 0
+#endif
 #ifndef XS_SEAL_WPE
 #define XS_SEAL_WPE 1
 #endif
@@ -1133,7 +1136,15 @@ __device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, ui
                                            uint8_t* __restrict__ ok, uint32_t* lds) {
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63u;
   // wave-uniform block index
-  const uint64_t blk = (uint64_t)blockIdx.x * 4u + (uint64_t)__builtin_amdgcn_readfirstlane(wave);
+#if XS_XCD_REMAP
+  // workgroups are dealt round-robin over the 8 XCDs: give each XCD one contiguous range of
+  // blocks (bijective for any grid size) so its L2 / TLB working set moves linearly
+  const uint32_t nwg = gridDim.x, q = nwg >> 3, rem = nwg & 7u, xcd = blockIdx.x & 7u;
+  const uint32_t wg = (xcd < rem ? xcd * (q + 1u) : rem * (q + 1u) + (xcd - rem) * q) + (blockIdx.x >> 3);
+#else
+  const uint32_t wg = blockIdx.x;
+#endif
+  const uint64_t blk = (uint64_t)wg * 4u + (uint64_t)__builtin_amdgcn_readfirstlane(wave);
   if (blk >= nblocks) return;
   const BlockKey* bk = keys + blk;
   if (bk->flags) {  // rejected descriptor: write nothing
