@@ -28,9 +28,19 @@
 #include <stdint.h>
 
 #include "xs_internal.h"
+#include "xs_salsa_lazy.h"
 
 // XS_SEAL_WPE / XS_OPEN_WPE: minimum waves per SIMD the register allocator must allow
 // (amdgpu_waves_per_eu) for the seal / open kernels.
+#ifndef XS_SALSA_LAZY  // Salsa20 double rounds with deferred XORs (v_xad_u32 / v_bitop3_b32)
+#define XS_SALSA_LAZY 1
+#endif
+#ifndef XS_ABL_NOMFMA  // diagnostic ablation only (wrong tags): skip the matrix-core Poly1305 MFMAs
+#define XS_ABL_NOMFMA 0
+#endif
+#ifndef XS_ABL_NOMEM  // diagnostic ablation only (wrong output): full blocks skip their HBM loads/stores
+#define XS_ABL_NOMEM 0
+#endif
 #ifndef XS_XCD_REMAP
 #define XS_XCD_REMAP 0
 #endif
@@ -174,6 +184,22 @@ __device__ __forceinline__ void salsa20_block_pre(const SalsaPre& p, uint32_t ct
   x[13] = p.x13 ^ rotl(x[12] + p.x15, 9);
   x[14] = p.x14 ^ rotl(x[13] + x[12], 13);
   x[15] = p.x15 ^ rotl(x[14] + x[13], 18);
+#if XS_SALSA_LAZY
+  // double rounds 2..10 with deferred XORs (xs_salsa_lazy.h): word i is b[i] ^ t[i] when bit
+  // i of XS_LAZY_MASK is set, else b[i]; the feed-forward absorbs the pending XOR (v_xad_u32)
+  uint32_t t[16];
+  xs_salsa_dr_lazy_enter(x, t);
+#pragma unroll 1
+  for (int i = 0; i < 8; i++) xs_salsa_dr_lazy(x, t);
+  const uint32_t in[16] = {SIG0, p.k[0], p.k[1], p.k[2], p.k[3], SIG1, p.n0, p.n1,
+                           ctr,  0u,     SIG2,   p.k[4], p.k[5], p.k[6], p.k[7], SIG3};
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    if ((XS_LAZY_MASK >> i) & 1u) out[i] = xs_xad(x[i], t[i], in[i]);
+    else out[i] = x[i] + in[i];
+  }
+  return;
+#endif
   salsa_rounds9(x);
   out[0] = x[0] + SIG0;
   out[1] = x[1] + p.k[0];
@@ -1022,7 +1048,7 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
     const uint32_t off = 64u * K;  // from 32 bytes before the block: never negative
 #pragma unroll
     for (int j = 0; j < 4; j++)
-      if (j >= 2 || !key_slots) {
+      if ((j >= 2 || !key_slots) && !XS_ABL_NOMEM) {
         __builtin_amdgcn_global_load_lds(pin_m32 + off + 16 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
       }
     uint32_t ks[16];
@@ -1039,7 +1065,7 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
     for (int i = 0; i < 16; i++) o[i] = d[i] ^ ks[i];
 #pragma unroll
     for (int j = 0; j < 4; j++)
-      if (j >= 2 || !key_slots) {
+      if ((j >= 2 || !key_slots) && (!XS_ABL_NOMEM || o[4 * j] == 0x12345678u)) {
         *reinterpret_cast<uint4*>(pout_m32 + off + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
       }
     // A operands of row 4u + kg for both output halves
@@ -1060,7 +1086,13 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
 #pragma unroll
       for (int i = 0; i < 4; i++) B[i] = (int)(cw[4 * j + i] ^ 0x80808080u);
 #pragma unroll
-      for (int mt = 0; mt < 2; mt++) acc[j][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[mt], B, acc[j][mt], 0, 0, 0);
+      for (int mt = 0; mt < 2; mt++) {
+#if XS_ABL_NOMFMA
+        acc[j][mt] += A[mt] ^ B;
+#else
+        acc[j][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[mt], B, acc[j][mt], 0, 0, 0);
+#endif
+      }
     }
   }
   // ---- transpose the partial words through the (now free) staging slot: lane (n, kg) holds,

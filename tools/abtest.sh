@@ -10,8 +10,9 @@ mkdir -p $D
 AREF=${AREF:-HEAD}
 if [ "$AREF" = tree ]; then
   cp rclone_amd/csrc/xs_kernels.hip $D/a_src.hip
-  cp rclone_amd/csrc/xs_internal.h $D/
+  cp rclone_amd/csrc/*.h $D/
 else
+  for h in $(git ls-tree --name-only "$AREF" rclone_amd/csrc/ | grep '\.h$'); do git show "$AREF":$h > $D/$(basename $h); done
   git show "$AREF":rclone_amd/csrc/xs_kernels.hip > $D/a_src.hip
   git show "$AREF":rclone_amd/csrc/xs_internal.h > $D/xs_internal.h
 fi
