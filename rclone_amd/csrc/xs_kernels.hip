@@ -38,6 +38,15 @@
 #ifndef XS_ABL_NOMFMA  // diagnostic ablation only (wrong tags): skip the matrix-core Poly1305 MFMAs
 #define XS_ABL_NOMFMA 0
 #endif
+#ifndef XS_LD_COAL  // staging loads read 1 KiB contiguous per wave instruction
+#define XS_LD_COAL 1
+#endif
+#ifndef XS_ST_COAL  // stores write 1 KiB contiguous per wave instruction (transposed through LDS)
+#define XS_ST_COAL 1
+#endif
+#if XS_ST_COAL && !XS_LD_COAL
+#error "XS_ST_COAL reuses the XS_LD_COAL staging layout"
+#endif
 #ifndef XS_ABL_NOMEM  // diagnostic ablation only (wrong output): full blocks skip their HBM loads/stores
 #define XS_ABL_NOMEM 0
 #endif
@@ -1014,7 +1023,7 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
   // loaded: zero them, so OPEN hashes zero bytes there and SEAL the keystream (keygen's corr)
   if (l == 0u) {
     *reinterpret_cast<uint4*>(wb) = make_uint4(0u, 0u, 0u, 0u);
-    *reinterpret_cast<uint4*>(wb + 256) = make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>(wb + (XS_LD_COAL ? 64 : 256)) = make_uint4(0u, 0u, 0u, 0u);
   }
   uint32_t k[8];
 #pragma unroll
@@ -1046,28 +1055,61 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
     const uint32_t K = 64u * u + l;
     const bool key_slots = K == 0u;  // chunks -2, -1: the Poly1305 key, not message
     const uint32_t off = 64u * K;  // from 32 bytes before the block: never negative
+#if XS_LD_COAL
+    // staging load j reads the wave's KiB j of this 4 KiB group contiguously: lane λ fetches
+    // 16-byte chunk 64j + 4(λ&15) + (λ>>4), landing at slot position λ, so lane L later finds
+    // its own chunks 4L+i at slot L>>4, positions (L&15) + 16i (conflict-free ds_read_b128)
+    const uint32_t ld_off = 64u * 64u * (uint32_t)u + 16u * (4u * (l & 15u) + (l >> 4));
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if ((j > 0 || u > 0 || (l & 47u) != 0u) && !XS_ABL_NOMEM)  // lanes 0 and 16 of load 0, u = 0: key slots
+        __builtin_amdgcn_global_load_lds(pin_m32 + ld_off + 1024 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
+#else
 #pragma unroll
     for (int j = 0; j < 4; j++)
       if ((j >= 2 || !key_slots) && !XS_ABL_NOMEM) {
         __builtin_amdgcn_global_load_lds(pin_m32 + off + 16 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
       }
+#endif
     uint32_t ks[16];
     salsa20_block_pre(pre, K, ks);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t d[16];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
+#if XS_LD_COAL
+      const uint4 v = *reinterpret_cast<const uint4*>(wb + 256 * (l >> 4) + 4 * (l & 15u) + 64 * j);
+#else
       const uint4 v = *reinterpret_cast<const uint4*>(wb + 256 * j + 4 * l);
+#endif
       d[4 * j] = v.x; d[4 * j + 1] = v.y; d[4 * j + 2] = v.z; d[4 * j + 3] = v.w;
     }
     uint32_t o[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) o[i] = d[i] ^ ks[i];
+#if XS_ST_COAL
+    // output through the staging slot: each lane puts its chunks back where it read its input
+    // from, then store j writes KiB j of the group contiguously (lane λ: chunk 64j + perm(λ))
+    {
+      uint4* mine = reinterpret_cast<uint4*>(wb + 256 * (l >> 4) + 4 * (l & 15u));
+#pragma unroll
+      for (int j = 0; j < 4; j++) mine[16 * j] = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
+      asm volatile("" ::: "memory");  // LDS ops of one wave execute in order
+      uint4 w[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) w[j] = *reinterpret_cast<const uint4*>(wb + 256 * j + 4 * l);
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if ((j > 0 || u > 0 || (l & 47u) != 0u) && (!XS_ABL_NOMEM || w[j].x == 0x12345678u))
+          *reinterpret_cast<uint4*>(pout_m32 + ld_off + 1024 * j) = w[j];
+    }
+#else
 #pragma unroll
     for (int j = 0; j < 4; j++)
       if ((j >= 2 || !key_slots) && (!XS_ABL_NOMEM || o[4 * j] == 0x12345678u)) {
         *reinterpret_cast<uint4*>(pout_m32 + off + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
       }
+#endif
     // A operands of row 4u + kg for both output halves
     const lds_u32* zr = zl + 48u * u;
     uint32_t z[9];
