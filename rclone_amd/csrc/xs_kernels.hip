@@ -38,14 +38,14 @@
 #ifndef XS_ABL_NOMFMA  // diagnostic ablation only (wrong tags): skip the matrix-core Poly1305 MFMAs
 #define XS_ABL_NOMFMA 0
 #endif
-#ifndef XS_LD_COAL  // staging loads read 1 KiB contiguous per wave instruction
-#define XS_LD_COAL 1
+#ifndef XS_ST_PERM  // output transpose with v_permlane{32,16}_swap instead of the LDS round trip
+#define XS_ST_PERM 0
 #endif
-#ifndef XS_ST_COAL  // stores write 1 KiB contiguous per wave instruction (transposed through LDS)
-#define XS_ST_COAL 1
+#ifndef XS_DBUF  // double-buffered staging (8 KiB per wave)
+#define XS_DBUF 0
 #endif
-#if XS_ST_COAL && !XS_LD_COAL
-#error "XS_ST_COAL reuses the XS_LD_COAL staging layout"
+#ifndef XS_ABL_NOSALSA  // diagnostic ablation only (wrong output): no Salsa20 keystream in the block loop
+#define XS_ABL_NOSALSA 0
 #endif
 #ifndef XS_ABL_NOMEM  // diagnostic ablation only (wrong output): full blocks skip their HBM loads/stores
 #define XS_ABL_NOMEM 0
@@ -714,7 +714,8 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
 #error "full blocks need the matrix-core path: keygen writes no T1/T2 tables for them"
 #endif
 #if XS_POLY_MFMA
-constexpr int WAVE_LDS_WORDS = 1024 + 768;  // 4 KiB staging + 3 KiB Toeplitz table
+constexpr int STAGE_WORDS = XS_DBUF ? 2048 : 1024;
+constexpr int WAVE_LDS_WORDS = STAGE_WORDS + 768;  // 4 KiB staging (x2 with XS_DBUF) + 3 KiB Toeplitz table
 #else
 constexpr int WAVE_LDS_WORDS = 1024;
 #endif
@@ -1019,11 +1020,17 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
     row[1] = make_uint4(__builtin_bswap32(w3), __builtin_bswap32(w2), __builtin_bswap32(w1), __builtin_bswap32(w0));
     row[2] = make_uint4(0u, 0u, 0u, 0u);
   }
-  // key slots (chunks -2, -1 = lane 0's first two staging chunks of super-iteration 0) are never
-  // loaded: zero them, so OPEN hashes zero bytes there and SEAL the keystream (keygen's corr)
+  // Staging layout (per 4 KiB group, one slot of 4 x 1 KiB): load j fetches KiB j of the group
+  // contiguously, lane λ taking 16-byte chunk 64j + perm(λ), perm(λ) = 4(λ&15) + (λ>>4), which
+  // lands at slot position λ; lane L then finds its own chunks 4L+i at KiB L>>4, positions
+  // (L&15) + 16i (conflict-free ds_read_b128).  Outputs go back through the same positions and
+  // leave in the load order, so every load and store wave-instruction covers 1 KiB.
+  // The key slots (chunks -2, -1 of the block = chunks 0, 1 of group 0 = lanes 0 and 16 of
+  // load 0) are never loaded or stored: zeroed here, OPEN hashes zero bytes there and SEAL the
+  // keystream (keygen's corr accounts for both).
   if (l == 0u) {
     *reinterpret_cast<uint4*>(wb) = make_uint4(0u, 0u, 0u, 0u);
-    *reinterpret_cast<uint4*>(wb + (XS_LD_COAL ? 64 : 256)) = make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>(wb + 64) = make_uint4(0u, 0u, 0u, 0u);
   }
   uint32_t k[8];
 #pragma unroll
@@ -1032,17 +1039,18 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
   // A window for output q = 16mt + n starts at Z byte 31 - q: words zlo .. zlo + 8 cover both
   // halves (mt = 1 at word zlo, mt = 0 at word zlo + 4), byte shift zsh
   const uint32_t zlo = (15u - n) >> 2, zsh = (31u - n) & 3u;
-  // input and output addressed from 32 bytes before the block (the key slots of
-  // super-iteration 0 lie there and are never touched): uniform base + 32-bit offset.
-  // (Raw buffer loads/stores here measured 3-4% slower for seal, neutral for open.)
+  // input and output addressed from 32 bytes before the block (uniform base + 32-bit offset;
+  // raw buffer loads/stores measured 3-4% slower for seal, neutral for open)
   const uint8_t* pin_m32 = pin - 32;
   uint8_t* pout_m32 = pout - 32;
+  const uint32_t lane_off = 16u * (4u * (l & 15u) + (l >> 4));  // perm(l) chunk, bytes
+  const bool not_key = (l & 47u) != 0u;                        // not lane 0 or 16
   // this lane's Z window in row kg, as an opaque LDS address so the per-row reads below use
   // one base register and ds_read2 offsets (otherwise the compiler splits off the slot offset)
   uint32_t zaddr = (uint32_t)(uintptr_t)((const lds_u32*)zb + 12u * kg + zlo);
   asm volatile("" : "+v"(zaddr));
   const lds_u32* zl = (const lds_u32*)(uintptr_t)zaddr;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own Z writes are visible
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own Z / zero writes are visible
   xs_v4i acc[4][2];
 #pragma unroll
   for (int j = 0; j < 4; j++)
@@ -1050,65 +1058,89 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
     for (int mt = 0; mt < 2; mt++)
 #pragma unroll
       for (int i = 0; i < 4; i++) acc[j][mt][i] = 1 << 24;
+#if XS_DBUF
+  // double-buffered staging: group u+1 is requested before group u's keystream is computed
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+    if ((j > 0 || not_key) && !XS_ABL_NOMEM)
+      __builtin_amdgcn_global_load_lds(pin_m32 + lane_off + 1024 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
+#endif
 #pragma unroll 1
   for (int u = 0; u < 16; u++) {
     const uint32_t K = 64u * u + l;
-    const bool key_slots = K == 0u;  // chunks -2, -1: the Poly1305 key, not message
-    const uint32_t off = 64u * K;  // from 32 bytes before the block: never negative
-#if XS_LD_COAL
-    // staging load j reads the wave's KiB j of this 4 KiB group contiguously: lane λ fetches
-    // 16-byte chunk 64j + 4(λ&15) + (λ>>4), landing at slot position λ, so lane L later finds
-    // its own chunks 4L+i at slot L>>4, positions (L&15) + 16i (conflict-free ds_read_b128)
-    const uint32_t ld_off = 64u * 64u * (uint32_t)u + 16u * (4u * (l & 15u) + (l >> 4));
+    const uint32_t goff = 4096u * (uint32_t)u + lane_off;
+#if XS_DBUF
+    uint32_t* sb = wb + 1024 * (u & 1);
+    if (u < 15) {
+      uint32_t* nb = wb + 1024 * ((u + 1) & 1);
 #pragma unroll
-    for (int j = 0; j < 4; j++)
-      if ((j > 0 || u > 0 || (l & 47u) != 0u) && !XS_ABL_NOMEM)  // lanes 0 and 16 of load 0, u = 0: key slots
-        __builtin_amdgcn_global_load_lds(pin_m32 + ld_off + 1024 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
+      for (int j = 0; j < 4; j++)
+        if (!XS_ABL_NOMEM)
+          __builtin_amdgcn_global_load_lds(pin_m32 + goff + 4096u + 1024 * j, (lds_void*)(nb + 256 * j), 16, 0, 0);
+    }
 #else
+    uint32_t* sb = wb;
 #pragma unroll
     for (int j = 0; j < 4; j++)
-      if ((j >= 2 || !key_slots) && !XS_ABL_NOMEM) {
-        __builtin_amdgcn_global_load_lds(pin_m32 + off + 16 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
-      }
+      if ((j > 0 || u > 0 || not_key) && !XS_ABL_NOMEM)
+        __builtin_amdgcn_global_load_lds(pin_m32 + goff + 1024 * j, (lds_void*)(sb + 256 * j), 16, 0, 0);
 #endif
     uint32_t ks[16];
+#if XS_ABL_NOSALSA
+#pragma unroll
+    for (int i = 0; i < 16; i++) ks[i] = K * (i + 1);
+#else
     salsa20_block_pre(pre, K, ks);
+#endif
+#if XS_DBUF
+    if (u < 15) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // group u landed; u+1 may be in flight
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    uint4* mine = reinterpret_cast<uint4*>(sb + 256 * (l >> 4) + 4 * (l & 15u));
     uint32_t d[16];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-#if XS_LD_COAL
-      const uint4 v = *reinterpret_cast<const uint4*>(wb + 256 * (l >> 4) + 4 * (l & 15u) + 64 * j);
-#else
-      const uint4 v = *reinterpret_cast<const uint4*>(wb + 256 * j + 4 * l);
-#endif
+      const uint4 v = mine[16 * j];
       d[4 * j] = v.x; d[4 * j + 1] = v.y; d[4 * j + 2] = v.z; d[4 * j + 3] = v.w;
     }
     uint32_t o[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) o[i] = d[i] ^ ks[i];
-#if XS_ST_COAL
-    // output through the staging slot: each lane puts its chunks back where it read its input
-    // from, then store j writes KiB j of the group contiguously (lane λ: chunk 64j + perm(λ))
-    {
-      uint4* mine = reinterpret_cast<uint4*>(wb + 256 * (l >> 4) + 4 * (l & 15u));
+#if XS_ST_PERM
+    {  // outputs leave in load order: 4x4 transpose of (16-lane row, chunk) with lane swaps --
+       // afterwards register chunk j of lane λ holds chunk λ>>4 of lane 16j + (λ&15), i.e.
+       // chunk 64j + perm(λ) of the group
+      uint32_t w[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) w[i] = o[i];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        auto a = __builtin_amdgcn_permlane32_swap(w[q], w[8 + q], false, false);
+        auto b = __builtin_amdgcn_permlane32_swap(w[4 + q], w[12 + q], false, false);
+        auto c = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+        auto e = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+        w[q] = c[0]; w[4 + q] = c[1]; w[8 + q] = e[0]; w[12 + q] = e[1];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if ((j > 0 || u > 0 || not_key) && (!XS_ABL_NOMEM || w[4 * j] == 0x12345678u))
+          *reinterpret_cast<uint4*>(pout_m32 + goff + 1024 * j) = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
+    }
+#else
+    {  // outputs back through the staging positions, then out in load order
 #pragma unroll
       for (int j = 0; j < 4; j++) mine[16 * j] = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
       asm volatile("" ::: "memory");  // LDS ops of one wave execute in order
       uint4 w[4];
 #pragma unroll
-      for (int j = 0; j < 4; j++) w[j] = *reinterpret_cast<const uint4*>(wb + 256 * j + 4 * l);
+      for (int j = 0; j < 4; j++) w[j] = *reinterpret_cast<const uint4*>(sb + 256 * j + 4 * l);
 #pragma unroll
       for (int j = 0; j < 4; j++)
-        if ((j > 0 || u > 0 || (l & 47u) != 0u) && (!XS_ABL_NOMEM || w[j].x == 0x12345678u))
-          *reinterpret_cast<uint4*>(pout_m32 + ld_off + 1024 * j) = w[j];
+        if ((j > 0 || u > 0 || not_key) && (!XS_ABL_NOMEM || w[j].x == 0x12345678u))
+          *reinterpret_cast<uint4*>(pout_m32 + goff + 1024 * j) = w[j];
     }
-#else
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-      if ((j >= 2 || !key_slots) && (!XS_ABL_NOMEM || o[4 * j] == 0x12345678u)) {
-        *reinterpret_cast<uint4*>(pout_m32 + off + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
-      }
 #endif
     // A operands of row 4u + kg for both output halves
     const lds_u32* zr = zl + 48u * u;
@@ -1235,7 +1267,7 @@ __device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, ui
   P5 h;
   h.v[0] = h.v[1] = h.v[2] = h.v[3] = h.v[4] = 0;
 #if XS_POLY_MFMA
-  if (n == XS_BLOCK_DATA) crypt_block_mfma<SEAL>(bk, pin, pout, wb, wb + 1024, h);
+  if (n == XS_BLOCK_DATA) crypt_block_mfma<SEAL>(bk, pin, pout, wb, wb + STAGE_WORDS, h);
 #else
   if (n == XS_BLOCK_DATA) crypt_block<SEAL, true>(bk, pin, pout, n, wb, h);
 #endif
