@@ -142,6 +142,15 @@ int xs_engine_open(xs_engine *e, const uint8_t key[32], const uint8_t nonce0[24]
  * pays off for many objects per call (hundreds+), not for one large stream. */
 int xs_engine_seal_md5(xs_engine *e, const uint8_t key[32], uint64_t nobj, const uint8_t *nonces,
                        const uint64_t *offs, const uint64_t *lens, const void *plain, uint8_t *md5);
+/* Fs.put of many whole objects at once (rclone sync/copy of a tree into crypt): the same
+ * seal + ciphertext MD5 as xs_engine_seal_md5, and the wire bodies come back too, packed into
+ * `body`: object i's body (rc_encrypted_size(len) - 32 bytes: tag||ct per block, no header)
+ * starts at the sum over k < i of round16(body bytes of object k).  One D2H per group.
+ * xs_put_body_bytes gives the total packed size for the `body` buffer (pinned for speed). */
+int xs_engine_put_batch(xs_engine *e, const uint8_t key[32], uint64_t nobj, const uint8_t *nonces,
+                        const uint64_t *offs, const uint64_t *lens, const void *plain, void *body,
+                        uint8_t *md5);
+uint64_t xs_put_body_bytes(uint64_t nobj, const uint64_t *lens);
 /* Cross-caller coalescing (default on; env XS_ENGINE_COALESCE=0 or this call turns it off):
  * concurrent xs_engine_seal/xs_engine_open callers whose request fits one engine batch are
  * packed into one combined GPU batch (group commit: the first caller in leads, the others

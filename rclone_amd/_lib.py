@@ -55,6 +55,8 @@ _SIGS = [
     ("xs_engine_seal", ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, u64, vp, u64, vp]),
     ("xs_engine_open", ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, u64, vp, u64, vp, vp]),
     ("xs_engine_seal_md5", ctypes.c_int, [vp, ctypes.c_char_p, u64, vp, vp, vp, vp, vp]),
+    ("xs_engine_put_batch", ctypes.c_int, [vp, ctypes.c_char_p, u64, vp, vp, vp, vp, vp, vp]),
+    ("xs_put_body_bytes", u64, [u64, vp]),
     ("xs_engine_set_coalesce", None, [vp, ctypes.c_int]),
     ("xs_engine_stats", None, [vp, vp]),
     ("xs_host_alloc", vp, [ctypes.c_size_t]),

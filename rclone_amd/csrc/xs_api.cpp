@@ -709,8 +709,11 @@ static uint64_t body_bytes(uint64_t plain_len) {
   return plain_len + nb * XS_BLOCK_HDR;
 }
 
-extern "C" int xs_engine_seal_md5(xs_engine* e, const uint8_t key[32], uint64_t nobj, const uint8_t* nonces,
-                                  const uint64_t* offs, const uint64_t* lens, const void* plain, uint8_t* md5) {
+// Seal + MD5 of whole objects in groups of ~budget plaintext bytes; with `body` the wire
+// bodies also come back (packed: object i at xs_put_body_offset of i, one D2H per group).
+static int seal_md5_impl(xs_engine* e, const uint8_t key[32], uint64_t nobj, const uint8_t* nonces,
+                         const uint64_t* offs, const uint64_t* lens, const void* plain, uint8_t* md5,
+                         uint8_t* body) {
   if (nobj == 0) return XS_OK;
   if (!e || !key || !nonces || !offs || !lens || !md5) {
     set_error("xs_engine_seal_md5: null argument");
@@ -729,10 +732,11 @@ extern "C" int xs_engine_seal_md5(xs_engine* e, const uint8_t key[32], uint64_t 
   hipStream_t st = e->slots[0].s;
   auto& hb = e->hb;
   // groups of whole objects, ~budget plaintext bytes each (MD5 is sequential per object)
-  const uint64_t budget = std::max<uint64_t>((uint64_t)e->batch * XS_BLOCK_DATA * 16, 256ull << 20);
+  // large groups: the MD5 of a group takes as long as its largest object (one lane each)
+  const uint64_t budget = std::max<uint64_t>((uint64_t)e->batch * XS_BLOCK_DATA * 16, 4096ull << 20);
   std::vector<xs_block_desc> desc;
   std::vector<xs_md5_desc> mdesc;
-  uint64_t o0 = 0;
+  uint64_t o0 = 0, body_pos = 0;
   while (o0 < nobj) {
     uint64_t o1 = o0, lo = UINT64_MAX, hi = 0, bsum = 0, nblk = 0;
     while (o1 < nobj) {
@@ -792,11 +796,34 @@ extern "C" int xs_engine_seal_md5(xs_engine* e, const uint8_t key[32], uint64_t 
     err = launch_md5((const xs_md5_desc*)hb.d_mdesc, ng, hb.d_body, bsum, hb.d_digest, nullptr, st);
     if (err != hipSuccess) return hip_fail(err, "md5");
     err = hipMemcpyAsync(md5 + 16 * o0, hb.d_digest, ng * 16, hipMemcpyDeviceToHost, st);
+    if (err == hipSuccess && body && w) err = hipMemcpyAsync(body + body_pos, hb.d_body, w, hipMemcpyDeviceToHost, st);
     if (err != hipSuccess) return hip_fail(err, "D2H");
+    body_pos += w;
     // the host-side descriptor vectors are reused next group: wait for this group's copies
     err = hipStreamSynchronize(st);
     if (err != hipSuccess) return hip_fail(err, "engine stream");
     o0 = o1;
   }
   return XS_OK;
+}
+
+extern "C" int xs_engine_seal_md5(xs_engine* e, const uint8_t key[32], uint64_t nobj, const uint8_t* nonces,
+                                  const uint64_t* offs, const uint64_t* lens, const void* plain, uint8_t* md5) {
+  return seal_md5_impl(e, key, nobj, nonces, offs, lens, plain, md5, nullptr);
+}
+
+extern "C" uint64_t xs_put_body_bytes(uint64_t nobj, const uint64_t* lens) {
+  uint64_t w = 0;
+  for (uint64_t i = 0; i < nobj; i++) w += (body_bytes(lens[i]) + 15) & ~15ull;
+  return w;
+}
+
+extern "C" int xs_engine_put_batch(xs_engine* e, const uint8_t key[32], uint64_t nobj, const uint8_t* nonces,
+                                   const uint64_t* offs, const uint64_t* lens, const void* plain, void* body,
+                                   uint8_t* md5) {
+  if (nobj && !body) {
+    set_error("xs_engine_put_batch: null body");
+    return XS_ERR_INVALID;
+  }
+  return seal_md5_impl(e, key, nobj, nonces, offs, lens, plain, md5, (uint8_t*)body);
 }

@@ -1,0 +1,506 @@
+// BASELINE configs[4] end-to-end harness: `rclone sync <local tree> crypt:` with crypt over an
+// in-memory remote (backend/memory), then `rclone cryptcheck`, in one process, through the C ABI
+// the Go side would bind (include/rclone_crypt_gpu.h).  Diagnostic / measurement tool, not the
+// product; the crypt work runs on the GPU through librclone_crypt.so.
+//
+// Flow (reference: crypt.go:497-563 Fs.put, memory.go:580-588 Object.Hash, crypt.go:784-852 +
+// cmd/cryptcheck/cryptcheck.go:67-117):
+//   tree   : files with log-uniform sizes in [4 KiB, 8 MiB] (+ 0/1/65536/65537-byte edge files),
+//            SplitMix64 content, written under --dir (page cache: the local backend's reads
+//            come from memory, as in a warm rclone run).
+//   sync   : batch mode (default) -- groups of whole files are read in parallel into a pinned
+//            staging buffer and handed to xs_engine_put_batch: one H2D, seal + MD5 of the crypt
+//            file on the GPU (the hash crypt.put tees off the ciphertext), the wire bodies D2H
+//            straight into the memory remote's (pinned) arena.  Two lanes (two engines) overlap
+//            one group's file reads and PCIe with the other's.
+//            stream mode (--mode stream) -- the reference's per-object shape: --transfers
+//            threads each run rc_encrypt_data over the open file (GPU behind the encrypter,
+//            cross-caller coalescing) and tee an MD5 of the ciphertext on the CPU.
+//            Either way crypt.put then compares the tee hash with the remote's Object.Hash
+//            (CPU MD5 of the stored bytes, cached) unless --check-dst-hash 0.
+//   check  : cryptcheck -- every local file re-sealed with the nonce read back from the stored
+//            header and MD5'd on the GPU (xs_engine_seal_md5), compared with the remote's hash.
+//   verify : sampled objects decrypted back through rc_decrypt_data (GPU) and compared with the
+//            local bytes; one stored object corrupted -> cryptcheck must flag exactly that one.
+// Prints one JSON line.
+//   usage: e2e_sync [--gib G] [--dir D] [--transfers T] [--mode batch|stream]
+//                   [--check-dst-hash 0|1] [--group-mib M] [--lanes L] [--keep]
+#include <fcntl.h>
+#include <sys/random.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../include/rclone_crypt_gpu.h"
+
+// ---------------------------------------------------------------- MD5 (RFC 1321), host
+struct Md5 {
+  uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+  uint8_t buf[64];
+  uint64_t n = 0;
+  static uint32_t rol(uint32_t x, int c) { return (x << c) | (x >> (32 - c)); }
+  void block(const uint8_t* p) {
+    static const uint32_t K[64] = {
+        0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
+        0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
+        0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+        0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
+        0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
+        0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+        0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+        0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+    static const int R[16] = {7, 12, 17, 22, 5, 9, 14, 20, 4, 11, 16, 23, 6, 10, 15, 21};
+    uint32_t m[16];
+    memcpy(m, p, 64);  // little-endian host
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
+    for (int i = 0; i < 64; i++) {
+      uint32_t f;
+      int g;
+      if (i < 16) { f = (b & c) | (~b & d); g = i; }
+      else if (i < 32) { f = (d & b) | (~d & c); g = (5 * i + 1) & 15; }
+      else if (i < 48) { f = b ^ c ^ d; g = (3 * i + 5) & 15; }
+      else { f = c ^ (b | ~d); g = (7 * i) & 15; }
+      const uint32_t t = d;
+      d = c;
+      c = b;
+      b = b + rol(a + f + K[i] + m[g], R[(i >> 4) * 4 + (i & 3)]);
+      a = t;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d;
+  }
+  void update(const uint8_t* p, size_t len) {
+    size_t have = n & 63;
+    n += len;
+    if (have) {
+      const size_t k = std::min(len, 64 - have);
+      memcpy(buf + have, p, k);
+      p += k;
+      len -= k;
+      if (have + k < 64) return;
+      block(buf);
+    }
+    for (; len >= 64; p += 64, len -= 64) block(p);
+    memcpy(buf, p, len);
+  }
+  void final(uint8_t out[16]) {
+    const uint64_t bits = n * 8;
+    const uint8_t one = 0x80, zero = 0;
+    update(&one, 1);
+    while ((n & 63) != 56) update(&zero, 1);
+    uint8_t lb[8];
+    for (int i = 0; i < 8; i++) lb[i] = (uint8_t)(bits >> (8 * i));
+    update(lb, 8);
+    memcpy(out, h, 16);
+  }
+};
+
+// ---------------------------------------------------------------- helpers
+static double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static uint64_t splitmix(uint64_t& s) {
+  uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static void parallel_for(size_t n, int threads, const std::function<void(size_t)>& f) {
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < std::max(1, threads); t++)
+    th.emplace_back([&] {
+      for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+    });
+  for (auto& t : th) t.join();
+}
+static bool read_file(const std::string& path, uint8_t* dst, uint64_t len) {
+  const int fd = open(path.c_str(), O_RDONLY);
+  if (fd < 0) return false;
+  uint64_t got = 0;
+  while (got < len) {
+    const ssize_t k = pread(fd, dst + got, len - got, (off_t)got);
+    if (k <= 0) break;
+    got += (uint64_t)k;
+  }
+  close(fd);
+  return got == len;
+}
+static uint64_t body_bytes(uint64_t plain) { return plain + ((plain + 65535) / 65536) * 16; }
+static uint64_t r16(uint64_t x) { return (x + 15) & ~15ull; }
+static const uint8_t kMagic[8] = {'R', 'C', 'L', 'O', 'N', 'E', 0, 0};
+
+// memory remote (backend/memory): objects keep header + body bytes and a lazily cached MD5
+struct Obj {
+  std::string name;
+  uint64_t size = 0;         // plaintext size (local file)
+  uint8_t header[32];        // magic || nonce
+  uint8_t* body = nullptr;   // wire body in the arena
+  uint64_t body_len = 0;
+  uint8_t tee[16];           // crypt.put's hash of the ciphertext stream
+  uint8_t dst[16];           // Object.Hash (memory.go:580-588), computed on demand
+  bool dst_ok = false;
+};
+static void dst_hash(Obj& o) {
+  if (o.dst_ok) return;
+  Md5 m;
+  m.update(o.header, 32);
+  m.update(o.body, o.body_len);
+  m.final(o.dst);
+  o.dst_ok = true;
+}
+
+// rc_reader over a file descriptor (ReadFill semantics are done by the rc_* layer)
+struct FdReader {
+  int fd;
+};
+static int64_t fd_read(void* u, uint8_t* p, int64_t n, int32_t* err) {
+  const ssize_t k = read(((FdReader*)u)->fd, p, (size_t)n);
+  if (k < 0) {
+    *err = RC_USER_BASE + 1;
+    return 0;
+  }
+  *err = k == 0 ? RC_EOF : RC_NIL;
+  return k;
+}
+static int32_t fd_close(void* u) {
+  close(((FdReader*)u)->fd);
+  return RC_NIL;
+}
+struct MemReader {
+  const uint8_t* a;
+  uint64_t na;
+  const uint8_t* b;
+  uint64_t nb, pos;
+};
+static int64_t mem_read(void* u, uint8_t* p, int64_t n, int32_t* err) {
+  MemReader* m = (MemReader*)u;
+  int64_t k = 0;
+  while (k < n && m->pos < m->na + m->nb) {
+    const bool first = m->pos < m->na;
+    const uint8_t* src = first ? m->a + m->pos : m->b + (m->pos - m->na);
+    const uint64_t avail = first ? m->na - m->pos : m->na + m->nb - m->pos;
+    const uint64_t c = std::min<uint64_t>(avail, (uint64_t)(n - k));
+    memcpy(p + k, src, c);
+    k += (int64_t)c;
+    m->pos += c;
+  }
+  *err = m->pos >= m->na + m->nb ? RC_EOF : RC_NIL;
+  return k;
+}
+static int32_t mem_close(void*) { return RC_NIL; }
+
+int main(int argc, char** argv) {
+  double gib = 8.0;
+  std::string dir = "/tmp/rc_e2e_src", mode = "batch";
+  int transfers = 16, check_dst = 1, keep = 0, nlanes = 4;
+  uint64_t group_mib = 4096;
+  for (int i = 1; i < argc; i++) {
+    std::string a = argv[i];
+    auto nx = [&] { return std::string(i + 1 < argc ? argv[++i] : ""); };
+    if (a == "--gib") gib = atof(nx().c_str());
+    else if (a == "--dir") dir = nx();
+    else if (a == "--transfers") transfers = atoi(nx().c_str());
+    else if (a == "--mode") mode = nx();
+    else if (a == "--check-dst-hash") check_dst = atoi(nx().c_str());
+    else if (a == "--group-mib") group_mib = strtoull(nx().c_str(), nullptr, 10);
+    else if (a == "--keep") keep = 1;
+    else if (a == "--lanes") nlanes = std::max(1, atoi(nx().c_str()));
+    else {
+      fprintf(stderr, "unknown argument %s\n", a.c_str());
+      return 2;
+    }
+  }
+  if (mode != "batch" && mode != "stream") return 2;
+  // ---- local tree
+  std::vector<Obj> objs;
+  {
+    uint64_t s = 0x5EED, total = 0;
+    const uint64_t edge[4] = {0, 1, 65536, 65537};
+    for (int i = 0; i < 4; i++) {
+      Obj o;
+      o.size = edge[i];
+      objs.push_back(o);
+      total += edge[i];
+    }
+    const double lo = std::log(4096.0), hi = std::log(8.0 * 1048576.0);
+    while ((double)total < gib * 1073741824.0) {
+      const double u = (double)(splitmix(s) >> 11) * (1.0 / 9007199254740992.0);
+      Obj o;
+      o.size = (uint64_t)std::exp(lo + u * (hi - lo));
+      total += o.size;
+      objs.push_back(o);
+    }
+    for (size_t i = 0; i < objs.size(); i++) objs[i].name = dir + "/f" + std::to_string(i);
+  }
+  mkdir(dir.c_str(), 0755);
+  uint64_t total = 0;
+  for (auto& o : objs) total += o.size;
+  const double tg0 = now();
+  parallel_for(objs.size(), transfers, [&](size_t i) {
+    std::vector<uint8_t> b(objs[i].size);
+    uint64_t s = 0xF11E0000ull + i;
+    for (uint64_t k = 0; k < b.size(); k += 8) {
+      const uint64_t v = splitmix(s);
+      memcpy(b.data() + k, &v, std::min<uint64_t>(8, b.size() - k));
+    }
+    const int fd = open(objs[i].name.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0 || write(fd, b.data(), b.size()) != (ssize_t)b.size()) {
+      fprintf(stderr, "cannot write %s\n", objs[i].name.c_str());
+      exit(1);
+    }
+    close(fd);
+  });
+  const double t_gen = now() - tg0;
+
+  int32_t err = 0;
+  rc_cipher* c = rc_cipher_new("potato", "", &err);
+  if (!c) {
+    fprintf(stderr, "rc_cipher_new failed %d\n", err);
+    return 1;
+  }
+  uint8_t key[32], nk[32], nt[16];
+  rc_cipher_keys(c, key, nk, nt);
+  // memory remote arena (pinned, so D2H lands in it directly)
+  std::vector<uint64_t> lens(objs.size()), boff(objs.size());
+  uint64_t arena_bytes = 0;
+  for (size_t i = 0; i < objs.size(); i++) {
+    lens[i] = objs[i].size;
+    boff[i] = arena_bytes;
+    arena_bytes += r16(body_bytes(objs[i].size));
+  }
+  uint8_t* arena = (uint8_t*)xs_host_alloc(arena_bytes ? arena_bytes : 16);
+  if (!arena) {
+    fprintf(stderr, "arena alloc failed: %s\n", xs_last_error());
+    return 1;
+  }
+  for (size_t i = 0; i < objs.size(); i++) {
+    objs[i].body = arena + boff[i];
+    objs[i].body_len = body_bytes(objs[i].size);
+  }
+  // groups of whole files, <= group_mib of plaintext (a larger file is a group of its own)
+  std::vector<std::pair<size_t, size_t>> groups;
+  for (size_t i = 0; i < objs.size();) {
+    size_t j = i;
+    uint64_t g = 0;
+    while (j < objs.size() && (j == i || g + r16(objs[j].size) <= (group_mib << 20))) g += r16(objs[j++].size);
+    groups.push_back({i, j});
+    i = j;
+  }
+  uint64_t max_group = 0;
+  for (auto& g : groups) {
+    uint64_t b = 0;
+    for (size_t i = g.first; i < g.second; i++) b += r16(objs[i].size);
+    max_group = std::max(max_group, b);
+  }
+  std::vector<uint8_t> nonces(24 * objs.size());
+  if (getrandom(nonces.data(), nonces.size(), 0) != (ssize_t)nonces.size()) return 1;  // crypto/rand
+  for (size_t i = 0; i < objs.size(); i++) {
+    memcpy(objs[i].header, kMagic, 8);
+    memcpy(objs[i].header + 8, nonces.data() + 24 * i, 24);
+  }
+  const int lanes = nlanes;
+  std::vector<xs_engine*> eng(lanes);
+  std::vector<uint8_t*> stage(lanes);
+  for (int l = 0; l < lanes; l++) {
+    eng[l] = xs_engine_create(0, 256, 1);
+    stage[l] = (uint8_t*)xs_host_alloc(max_group ? max_group : 16);
+    if (!eng[l] || !stage[l]) {
+      fprintf(stderr, "engine/staging: %s\n", xs_last_error());
+      return 1;
+    }
+  }
+  std::atomic<int> failures{0};
+  std::mutex tmu;
+  double t_read = 0, t_gpu = 0;  // summed over lanes (per phase: reset below)
+  // one group through one lane: parallel file reads into staging, then `gpu` on it
+  auto run_groups = [&](const std::function<void(int lane, size_t g, const std::vector<uint64_t>& offs)>& gpu) {
+    std::vector<std::thread> th;
+    for (int l = 0; l < lanes; l++)
+      th.emplace_back([&, l] {
+        for (size_t g = l; g < groups.size(); g += lanes) {
+          const size_t a = groups[g].first, b = groups[g].second;
+          std::vector<uint64_t> offs(b - a);
+          uint64_t pos = 0;
+          for (size_t i = a; i < b; i++) {
+            offs[i - a] = pos;
+            pos += r16(objs[i].size);
+          }
+          const double t0 = now();
+          parallel_for(b - a, std::max(1, transfers / lanes), [&](size_t k) {
+            if (!read_file(objs[a + k].name, stage[l] + offs[k], objs[a + k].size)) failures++;
+          });
+          const double t1 = now();
+          gpu(l, g, offs);
+          std::lock_guard<std::mutex> lk(tmu);
+          t_read += t1 - t0;
+          t_gpu += now() - t1;
+        }
+      });
+    for (auto& t : th) t.join();
+  };
+  // ---- sync
+  double t_sync = 0, t_dst = 0, sync_read = 0, sync_gpu = 0;
+  uint64_t put_mismatch = 0;
+  if (mode == "batch") {
+    const double t0 = now();
+    run_groups([&](int l, size_t g, const std::vector<uint64_t>& offs) {
+      const size_t a = groups[g].first, n = groups[g].second - a;
+      std::vector<uint8_t> md5(16 * n);
+      if (xs_engine_put_batch(eng[l], key, n, nonces.data() + 24 * a, offs.data(), lens.data() + a, stage[l],
+                              arena + boff[a], md5.data()) != XS_OK) {
+        fprintf(stderr, "put_batch: %s\n", xs_last_error());
+        failures++;
+        return;
+      }
+      for (size_t k = 0; k < n; k++) memcpy(objs[a + k].tee, md5.data() + 16 * k, 16);
+    });
+    t_sync = now() - t0;
+    sync_read = t_read;
+    sync_gpu = t_gpu;
+  } else {
+    const double t0 = now();
+    parallel_for(objs.size(), transfers, [&](size_t i) {
+      Obj& o = objs[i];
+      FdReader fr{open(o.name.c_str(), O_RDONLY)};
+      if (fr.fd < 0) {
+        failures++;
+        return;
+      }
+      rc_reader r{fd_read, nullptr, nullptr, &fr};  // the encrypter does not close its source
+      int32_t e = 0;
+      rc_encrypter* h = rc_encrypt_data(c, r, nonces.data() + 24 * i, &e);
+      if (!h) {
+        failures++;
+        return;
+      }
+      // memory backend Put reads the stream into its buffer; crypt.put tees the MD5
+      Md5 tee;
+      std::vector<uint8_t> ct(32 + o.body_len + 1);
+      uint64_t got = 0;
+      for (;;) {
+        const int64_t k = rc_encrypter_read(h, ct.data() + got, (int64_t)(ct.size() - got), &e);
+        got += (uint64_t)k;
+        if (e != RC_NIL || got == ct.size()) break;
+      }
+      rc_encrypter_free(h);
+      if ((e != RC_EOF && e != RC_NIL) || got != 32 + o.body_len) {
+        failures++;
+        return;
+      }
+      tee.update(ct.data(), got);
+      tee.final(o.tee);
+      memcpy(o.body, ct.data() + 32, o.body_len);
+      fd_close(&fr);
+    });
+    t_sync = now() - t0;
+  }
+  if (check_dst) {  // crypt.put: srcHash (tee) vs dstHash (the remote's MD5 of what it stored)
+    const double t0 = now();
+    std::atomic<uint64_t> bad{0};
+    parallel_for(objs.size(), transfers, [&](size_t i) {
+      dst_hash(objs[i]);
+      if (memcmp(objs[i].tee, objs[i].dst, 16)) bad++;
+    });
+    t_dst = now() - t0;
+    put_mismatch = bad;
+  }
+  // ---- cryptcheck: re-seal each local file with the stored nonce, MD5 on the GPU, compare
+  auto cryptcheck = [&](std::vector<uint8_t>& differ) {
+    differ.assign(objs.size(), 0);
+    run_groups([&](int l, size_t g, const std::vector<uint64_t>& offs) {
+      const size_t a = groups[g].first, n = groups[g].second - a;
+      std::vector<uint8_t> ns(24 * n), md5(16 * n);
+      for (size_t k = 0; k < n; k++) memcpy(ns.data() + 24 * k, objs[a + k].header + 8, 24);  // nonce from the remote
+      if (xs_engine_seal_md5(eng[l], key, n, ns.data(), offs.data(), lens.data() + a, stage[l], md5.data()) != XS_OK) {
+        failures++;
+        return;
+      }
+      for (size_t k = 0; k < n; k++) {
+        Obj& o = objs[a + k];
+        dst_hash(o);  // underlying object's hash (cached by put's check)
+        differ[a + k] = memcmp(md5.data() + 16 * k, o.dst, 16) != 0;
+      }
+    });
+  };
+  std::vector<uint8_t> differ;
+  t_read = t_gpu = 0;
+  const double tc0 = now();
+  cryptcheck(differ);
+  const double t_check = now() - tc0, check_read = t_read, check_gpu = t_gpu;
+  uint64_t ndiff = 0;
+  for (auto d : differ) ndiff += d;
+  // ---- verify: decrypt sampled objects through rc_decrypt_data and compare with the files
+  uint64_t verified = 0, verify_bad = 0;
+  for (size_t i = 0; i < objs.size(); i += std::max<size_t>(1, objs.size() / 64)) {
+    Obj& o = objs[i];
+    MemReader mr{o.header, 32, o.body, o.body_len, 0};
+    rc_reader r{mem_read, mem_close, nullptr, &mr};
+    int32_t e = 0;
+    rc_decrypter* d = rc_decrypt_data(c, r, &e);
+    std::vector<uint8_t> want(o.size), got(o.size + 1);
+    if (!d || !read_file(o.name, want.data(), o.size)) {
+      verify_bad++;
+      continue;
+    }
+    uint64_t n = 0;
+    for (;;) {
+      const int64_t k = rc_decrypter_read(d, got.data() + n, (int64_t)(got.size() - n), &e);
+      n += (uint64_t)k;
+      if (e != RC_NIL || n == got.size()) break;
+    }
+    rc_decrypter_close(d);
+    rc_decrypter_free(d);
+    if (n != o.size || memcmp(got.data(), want.data(), o.size) || (e != RC_EOF && e != RC_NIL)) verify_bad++;
+    verified++;
+  }
+  // corruption: flip one ciphertext byte of one stored object, drop its cached hash
+  size_t victim = objs.size() / 2;
+  while (victim < objs.size() && objs[victim].body_len < 100) victim++;
+  uint64_t flagged = 0;
+  bool only_victim = false;
+  if (victim < objs.size()) {
+    objs[victim].body[objs[victim].body_len / 2] ^= 0x01;
+    objs[victim].dst_ok = false;
+    std::vector<uint8_t> d2;
+    cryptcheck(d2);
+    for (auto d : d2) flagged += d;
+    only_victim = flagged == 1 && d2[victim];
+  }
+  const bool ok = failures == 0 && put_mismatch == 0 && ndiff == 0 && verify_bad == 0 && only_victim;
+  const double g = (double)total / 1073741824.0;
+  printf("{\"config\": \"configs[4] e2e: sync local tree -> crypt(memory), cryptcheck\", \"mode\": \"%s\", "
+         "\"objects\": %zu, \"gib\": %.3f, \"transfers\": %d, \"lanes\": %d, \"group_mib\": %llu, "
+         "\"sync_s\": %.3f, \"sync_GiB_s\": %.2f, \"dst_hash_s\": %.3f, \"sync_with_hash_check_GiB_s\": %.2f, "
+         "\"cryptcheck_s\": %.3f, \"cryptcheck_GiB_s\": %.2f, \"put_hash_mismatches\": %llu, "
+         "\"cryptcheck_differences\": %llu, \"verified_objects\": %llu, \"verify_failures\": %llu, "
+         "\"corruption_flagged\": %llu, \"tree_write_s\": %.2f, \"lane_seconds\": {\"sync_read\": %.3f, "
+         "\"sync_gpu\": %.3f, \"check_read\": %.3f, \"check_gpu\": %.3f}, \"ok\": %s}\n",
+         mode.c_str(), objs.size(), g, transfers, lanes, (unsigned long long)group_mib, t_sync, g / t_sync, t_dst,
+         check_dst ? g / (t_sync + t_dst) : 0.0, t_check, g / t_check, (unsigned long long)put_mismatch,
+         (unsigned long long)ndiff, (unsigned long long)verified, (unsigned long long)verify_bad,
+         (unsigned long long)flagged, t_gen, sync_read, sync_gpu, check_read, check_gpu, ok ? "true" : "false");
+  for (int l = 0; l < lanes; l++) {
+    xs_engine_destroy(eng[l]);
+    xs_host_free(stage[l]);
+  }
+  xs_host_free(arena);
+  rc_cipher_free(c);
+  if (!keep) {
+    for (auto& o : objs) unlink(o.name.c_str());
+    rmdir(dir.c_str());
+  }
+  return ok ? 0 : 1;
+}
