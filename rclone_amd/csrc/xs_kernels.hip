@@ -44,6 +44,9 @@
 #ifndef XS_DBUF  // double-buffered staging (8 KiB per wave)
 #define XS_DBUF 0
 #endif
+#ifndef XS_SPLIT_MAX  // batches up to this many blocks run four waves per block (latency)
+#define XS_SPLIT_MAX 256
+#endif
 #ifndef XS_ABL_NOSALSA  // diagnostic ablation only (wrong output): no Salsa20 keystream in the block loop
 #define XS_ABL_NOSALSA 0
 #endif
@@ -988,10 +991,17 @@ __device__ __forceinline__ P5 column_value(const uint64_t (&x)[8]) {
   return V;
 }
 
-template <bool SEAL>
-__device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk, const uint8_t* __restrict__ pin,
-                                                 uint8_t* __restrict__ pout, uint32_t* wb, uint32_t* zb, P5& h) {
+// NSPLIT = 1: the wave does all 16 super-iterations of its block.  NSPLIT = 4 (small batches,
+// latency): the block's four waves take four super-iterations each, their (linear) MFMA
+// accumulators are added through LDS and wave 0 finalises; returns whether this wave finalises.
+template <bool SEAL, int NSPLIT>
+__device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk, const uint8_t* __restrict__ pin,
+                                                 uint8_t* __restrict__ pout, uint32_t* wb, uint32_t* zb, P5& h,
+                                                 uint32_t wave, uint32_t* lds_all) {
+  static_assert(NSPLIT == 1 || NSPLIT == 4, "split factor");
   const uint32_t l = threadIdx.x & 63u, n = l & 15u, kg = l >> 4;
+  const int u_begin = NSPLIT == 1 ? 0 : 4 * (int)wave, u_end = u_begin + 16 / NSPLIT;
+  const bool lead = NSPLIT == 1 || wave == 0u;
   // ---- Z table: row p = l holds the signed digits D_0..D_16 of r^(64(63-p)) reversed,
   // Z[u] = D_{31-u} for 15 <= u <= 31, zero elsewhere (12 words per row).  W is stored
   // uncanonicalised (< 2^131): repack the limbs with carries, any representative works.
@@ -1057,8 +1067,9 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
 #pragma unroll
     for (int mt = 0; mt < 2; mt++)
 #pragma unroll
-      for (int i = 0; i < 4; i++) acc[j][mt][i] = 1 << 24;
+      for (int i = 0; i < 4; i++) acc[j][mt][i] = lead ? 1 << 24 : 0;  // the bias once per block
 #if XS_DBUF
+  static_assert(NSPLIT == 1, "XS_DBUF is a whole-block-per-wave variant");
   // double-buffered staging: group u+1 is requested before group u's keystream is computed
 #pragma unroll
   for (int j = 0; j < 4; j++)
@@ -1066,7 +1077,7 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
       __builtin_amdgcn_global_load_lds(pin_m32 + lane_off + 1024 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
 #endif
 #pragma unroll 1
-  for (int u = 0; u < 16; u++) {
+  for (int u = u_begin; u < u_end; u++) {
     const uint32_t K = 64u * u + l;
     const uint32_t goff = 4096u * (uint32_t)u + lane_off;
 #if XS_DBUF
@@ -1169,6 +1180,28 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
       }
     }
   }
+  if (NSPLIT > 1) {  // add the other waves' accumulators into wave 0's
+    if (!SEAL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // plaintext stores done before a zero-fill
+    __syncthreads();  // every wave is past its staging and Toeplitz reads
+    if (!lead) {
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) lds_all[(wave - 1u) * 2048u + (uint32_t)(8 * j + 4 * mt + i) * 64u + l] = acc[j][mt][i];
+    }
+    __syncthreads();
+    if (!lead) return false;
+#pragma unroll
+    for (int w = 0; w < NSPLIT - 1; w++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) acc[j][mt][i] += (int)lds_all[(uint32_t)w * 2048u + (uint32_t)(8 * j + 4 * mt + i) * 64u + l];
+  }
   // ---- transpose the partial words through the (now free) staging slot: lane (n, kg) holds,
   // for column 4n + j, the words at 2^(32(4mt + kg)); lane λ finalises column 4(λ&15) + (λ>>4)
   uint64_t* t64 = reinterpret_cast<uint64_t*>(wb);
@@ -1234,9 +1267,10 @@ __device__ __forceinline__ void crypt_block_mfma(const BlockKey* __restrict__ bk
   }
   pnorm(hs);
   h = hs;
+  return true;
 }
 
-template <bool SEAL>
+template <bool SEAL, int NSPLIT>
 __device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, uint64_t nblocks,
                                            const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                            uint8_t* __restrict__ ok, uint32_t* lds) {
@@ -1250,14 +1284,15 @@ __device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, ui
 #else
   const uint32_t wg = blockIdx.x;
 #endif
-  const uint64_t blk = (uint64_t)wg * 4u + (uint64_t)__builtin_amdgcn_readfirstlane(wave);
+  const uint64_t blk = NSPLIT == 1 ? (uint64_t)wg * 4u + (uint64_t)__builtin_amdgcn_readfirstlane(wave) : (uint64_t)wg;
   if (blk >= nblocks) return;
   const BlockKey* bk = keys + blk;
   if (bk->flags) {  // rejected descriptor: write nothing
-    if (!SEAL && l == 0) ok[blk] = 0;
+    if (!SEAL && l == 0 && (NSPLIT == 1 || wave == 0u)) ok[blk] = 0;
     return;
   }
   const uint32_t n = bk->len;
+  if (NSPLIT > 1 && n != XS_BLOCK_DATA && wave != 0u) return;  // a partial block: wave 0 alone
   const uint8_t* in = src + bk->src;
   uint8_t* out = dst + bk->dst;
   const uint8_t* pin = SEAL ? in : in + XS_BLOCK_HDR;
@@ -1267,8 +1302,11 @@ __device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, ui
   P5 h;
   h.v[0] = h.v[1] = h.v[2] = h.v[3] = h.v[4] = 0;
 #if XS_POLY_MFMA
-  if (n == XS_BLOCK_DATA) crypt_block_mfma<SEAL>(bk, pin, pout, wb, wb + STAGE_WORDS, h);
+  if (n == XS_BLOCK_DATA) {
+    if (!crypt_block_mfma<SEAL, NSPLIT>(bk, pin, pout, wb, wb + STAGE_WORDS, h, wave, lds)) return;
+  }
 #else
+  static_assert(NSPLIT == 1, "split mode needs the matrix-core Poly1305");
   if (n == XS_BLOCK_DATA) crypt_block<SEAL, true>(bk, pin, pout, n, wb, h);
 #endif
   else crypt_block<SEAL, false>(bk, pin, pout, n, wb, h);
@@ -1334,7 +1372,7 @@ xs_seal(const BlockKey* __restrict__ keys, uint64_t nblocks, const uint8_t* __re
         uint8_t* __restrict__ dst) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
   XS_PROBE_BEGIN
-  crypt_wave<true>(keys, nblocks, src, dst, nullptr, lds);
+  crypt_wave<true, 1>(keys, nblocks, src, dst, nullptr, lds);
   XS_PROBE_END
 }
 
@@ -1342,8 +1380,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XS_OPE
 xs_open(const BlockKey* __restrict__ keys, uint64_t nblocks, const uint8_t* __restrict__ src,
         uint8_t* __restrict__ dst, uint8_t* __restrict__ ok) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
-  crypt_wave<false>(keys, nblocks, src, dst, ok, lds);
+  crypt_wave<false, 1>(keys, nblocks, src, dst, ok, lds);
 }
+
+#if XS_POLY_MFMA
+// Small batches (latency: a lone ranged read, a few coalesced handles): one block per
+// workgroup, four waves on four super-iterations each.
+__global__ void __launch_bounds__(256) xs_seal_split(const BlockKey* __restrict__ keys, uint64_t nblocks,
+                                                     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
+  crypt_wave<true, 4>(keys, nblocks, src, dst, nullptr, lds);
+}
+
+__global__ void __launch_bounds__(256) xs_open_split(const BlockKey* __restrict__ keys, uint64_t nblocks,
+                                                     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                     uint8_t* __restrict__ ok) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
+  crypt_wave<false, 4>(keys, nblocks, src, dst, ok, lds);
+}
+#endif
 
 // SplitMix64 fill (synthetic benchmark objects generated in HBM).  Global word g of the stream
 // is mix(seed + (g+1)*golden); local 64 KiB block b of the buffer holds global block
@@ -1385,6 +1440,17 @@ void probe_read(unsigned long long* host, size_t n) {
 hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const uint8_t* src, uint8_t* dst,
                         uint8_t* ok, hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
+#if XS_POLY_MFMA
+  static const uint64_t split_max = [] {  // env XS_SPLIT_MAX overrides (A/B, 0 = never)
+    const char* v = getenv("XS_SPLIT_MAX");
+    return v ? strtoull(v, nullptr, 10) : (uint64_t)XS_SPLIT_MAX;
+  }();
+  if (nblocks <= split_max) {  // few blocks: four waves per block (shorter launch)
+    if (seal) hipLaunchKernelGGL(xs_seal_split, dim3((unsigned)nblocks), dim3(256), 0, stream, keys, nblocks, src, dst);
+    else hipLaunchKernelGGL(xs_open_split, dim3((unsigned)nblocks), dim3(256), 0, stream, keys, nblocks, src, dst, ok);
+    return hipGetLastError();
+  }
+#endif
   const unsigned grid = (unsigned)((nblocks + 3) / 4);  // four blocks (waves) per workgroup
   if (seal) hipLaunchKernelGGL(xs_seal, dim3(grid), dim3(256), 0, stream, keys, nblocks, src, dst);
   else hipLaunchKernelGGL(xs_open, dim3(grid), dim3(256), 0, stream, keys, nblocks, src, dst, ok);

@@ -142,3 +142,36 @@ def test_full_size_round_trip(dev):
         assert host_body[b].cpu().numpy().tobytes() == want, b
     # the device generator matches the host SplitMix64 generator
     assert host_plain[0, :4096].cpu().numpy().tobytes() == splitmix64_bytes(0x5EED, 4096)
+
+
+def test_split_and_wave_paths_agree():
+    # batches of <= XS_SPLIT_MAX (256) blocks run four waves per block (xs_seal_split /
+    # xs_open_split), larger ones one wave per block: same bytes, tags and verdicts
+    import torch
+    from rclone_amd import device
+    from rclone_amd.testdata import splitmix64_bytes
+    from oracle import pyoracle as orc
+    key = splitmix64_bytes(31, 32)
+    nonce0 = bytes([0xFE] + [0xFF] * 7 + list(splitmix64_bytes(32, 16)))  # carries from block 2
+    nbig = 300
+    plain = splitmix64_bytes(33, nbig * 65536 + 777)
+    tb = torch.from_numpy(np.frombuffer(plain, dtype=np.uint8).copy()).cuda()
+    body_big = device.seal_object(key, nonce0, tb)                      # 301 blocks: wave path
+    small = 200 * 65536
+    body_small = device.seal_object(key, nonce0, tb[:small].clone())    # 200 blocks: split path
+    one = device.seal_object(key, nonce0, tb[:65536].clone())           # 1 block: split path
+    torch.cuda.synchronize()
+    bb, bs = body_big.cpu().numpy().tobytes(), body_small.cpu().numpy().tobytes()
+    assert bs == bb[:200 * 65552]
+    assert one.cpu().numpy().tobytes() == bb[:65552]
+    assert bs[:3 * 65552] == orc.encrypt_file(plain[:3 * 65536], nonce0, key)[32:]
+    # open both ways, with a tampered block in each
+    for nb, body in ((200, body_small.clone()), (301, body_big.clone())):
+        body[65552 * 7 + 16 + 5] ^= 1
+        out, ok = device.open_object(key, nonce0, body)
+        torch.cuda.synchronize()
+        okn = ok.cpu().numpy()[:nb]
+        assert list(np.nonzero(okn == 0)[0]) == [7], nb
+        o = out.cpu().numpy().tobytes()
+        assert o[7 * 65536:8 * 65536] == bytes(65536)
+        assert o[:7 * 65536] == plain[:7 * 65536] and o[8 * 65536:nb * 65536 - 65536] == plain[8 * 65536:nb * 65536 - 65536]
