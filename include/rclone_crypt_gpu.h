@@ -142,7 +142,9 @@ int xs_engine_open(xs_engine *e, const uint8_t key[32], const uint8_t nonce0[24]
  * pays off for many objects per call (hundreds+), not for one large stream. */
 int xs_engine_seal_md5(xs_engine *e, const uint8_t key[32], uint64_t nobj, const uint8_t *nonces,
                        const uint64_t *offs, const uint64_t *lens, const void *plain, uint8_t *md5);
-/* Fs.put of many whole objects at once (rclone sync/copy of a tree into crypt): the same
+/* Fs.put of many whole objects at once (rclone sync/copy of a tree into crypt; replaces, per
+ * object, encryptData + the ciphertext MD5 tee of crypt.go:507-536 feeding the wrapped put):
+ * the same
  * seal + ciphertext MD5 as xs_engine_seal_md5, and the wire bodies come back too, packed into
  * `body`: object i's body (rc_encrypted_size(len) - 32 bytes: tag||ct per block, no header)
  * starts at the sum over k < i of round16(body bytes of object k).  One D2H per group.
