@@ -281,8 +281,13 @@ struct xs_engine {
     uint8_t* ok;
     int rc;
     bool done;
+    // zero-copy: in/out are pinned host memory the kernels can address directly (d_in/d_out)
+    bool zc;
+    uint64_t d_in, d_out;
+    uint64_t blk0;  // first block within its combined batch
   };
   bool coalesce = true;
+  bool zero_copy = true;  // pinned caller buffers go to the kernels directly (no staging copies)
   std::mutex qmu;
   std::condition_variable qcv;
   std::vector<Req*> queue;
@@ -293,6 +298,9 @@ struct xs_engine {
     uint8_t *in = nullptr, *out = nullptr, *ok = nullptr, *desc = nullptr;
     BlockKey* keys = nullptr;
     xs_block_desc* h_desc = nullptr;  // pinned
+    uint8_t* h_ok = nullptr;          // pinned: verdicts of a zero-copy batch
+    uint64_t d_h_desc = 0, d_h_ok = 0;  // their device addresses
+    bool zc = false;
     std::vector<Req*> batch;
     uint64_t blocks = 0;
     int rc = XS_OK;
@@ -311,6 +319,25 @@ struct xs_engine {
     size_t plain_cap = 0, body_cap = 0, desc_cap = 0, mdesc_cap = 0, digest_cap = 0, keys_cap = 0;
   } hb;
 };
+
+// Device address of pinned (page-locked, device-mapped) host memory, or false for anything else
+// (pageable memory, device memory): only such buffers are handed to the kernels directly.
+static bool host_dev_ptr(const void* p, uint64_t* dev) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory reports an error; clear it
+    return false;
+  }
+  if (a.type != hipMemoryTypeHost) return false;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess || !d) {
+    (void)hipGetLastError();
+    return false;
+  }
+  *dev = (uint64_t)(uintptr_t)d;
+  return true;
+}
 
 static bool grow(uint8_t** p, size_t* cap, size_t need) {
   if (*cap >= need) return true;
@@ -341,6 +368,7 @@ static void engine_free(xs_engine* e) {
     (void)hipFree(c.desc);
     (void)hipFree(c.keys);
     (void)hipHostFree(c.h_desc);
+    (void)hipHostFree(c.h_ok);
     if (c.done) (void)hipEventDestroy(c.done);
     if (c.s) (void)hipStreamDestroy(c.s);
   }
@@ -392,13 +420,16 @@ extern "C" xs_engine* xs_engine_create(int device, uint32_t batch_blocks, int ns
         hipMalloc(&c.ok, batch_blocks) != hipSuccess ||
         hipMalloc(&c.desc, (size_t)batch_blocks * sizeof(xs_block_desc)) != hipSuccess ||
         hipMalloc(&c.keys, (size_t)batch_blocks * sizeof(BlockKey)) != hipSuccess ||
-        hipHostMalloc(&c.h_desc, (size_t)batch_blocks * sizeof(xs_block_desc), hipHostMallocPortable) != hipSuccess) {
+        hipHostMalloc(&c.h_desc, (size_t)batch_blocks * sizeof(xs_block_desc), hipHostMallocPortable) != hipSuccess ||
+        hipHostMalloc(&c.h_ok, batch_blocks, hipHostMallocPortable) != hipSuccess ||
+        !host_dev_ptr(c.h_desc, &c.d_h_desc) || !host_dev_ptr(c.h_ok, &c.d_h_ok)) {
       set_error("xs_engine_create: device allocation failed");
       engine_free(e);
       return nullptr;
     }
   }
   if (const char* v = getenv("XS_ENGINE_COALESCE")) e->coalesce = atoi(v) != 0;
+  if (const char* v = getenv("XS_ENGINE_ZERO_COPY")) e->zero_copy = atoi(v) != 0;
   return e;
 }
 
@@ -540,6 +571,50 @@ static void nonce_plus(uint8_t out[24], const uint8_t n0[24], uint64_t x) {
 
 static NonceArg bounds_arg(uint64_t src_len, uint64_t dst_len);
 
+// Zero-copy form of a combined batch (descriptors already in the pinned h_desc, offsets from
+// the lowest caller input / output address): keygen reads the descriptors from host memory,
+// the crypt kernels read the callers' inputs and write their outputs over PCIe, verdicts land
+// in the pinned h_ok.  Two launches per direction run and one event -- no staging copies.
+static int engine_issue_zero_copy(xs_engine::CSlot& c, const std::vector<uint64_t>& blk0, uint64_t nblk) {
+  auto& batch = c.batch;
+  hipStream_t st = c.s;
+  uint64_t sbase = UINT64_MAX, dbase = UINT64_MAX, send = 0, dend = 0;
+  for (const auto* q : batch) {
+    sbase = std::min(sbase, q->d_in);
+    dbase = std::min(dbase, q->d_out);
+    send = std::max(send, q->d_in + q->in_len);
+    dend = std::max(dend, q->d_out + q->out_len);
+  }
+  NonceArg bounds = bounds_arg(send - sbase, dend - dbase);
+  bounds.n[4] = (uint32_t)(sbase & 15u);
+  bounds.n[5] = (uint32_t)(dbase & 15u);
+  const xs_block_desc* dd = (const xs_block_desc*)(uintptr_t)c.d_h_desc;
+  uint64_t nseal = 0;
+  hipError_t err = hipSuccess;
+  for (size_t r = 0; r < batch.size();) {  // one keygen per run of (direction, key)
+    size_t r1 = r + 1;
+    while (r1 < batch.size() && batch[r1]->seal == batch[r]->seal && !memcmp(batch[r1]->key, batch[r]->key, 32)) r1++;
+    const uint64_t b0 = blk0[r], b1 = r1 < batch.size() ? blk0[r1] : nblk;
+    err = launch_keygen(batch[r]->seal ? 2 : 3, key_arg(batch[r]->key), bounds, 0, 0, b1 - b0, dd + b0, c.keys + b0, st);
+    if (err != hipSuccess) return hip_fail(err, "zero-copy keygen");
+    if (batch[r]->seal) nseal = b1;
+    r = r1;
+  }
+  const uint8_t* src = (const uint8_t*)(uintptr_t)sbase;
+  uint8_t* dst = (uint8_t*)(uintptr_t)dbase;
+  if (nseal) {
+    err = launch_crypt(true, c.keys, nseal, src, dst, nullptr, st);
+    if (err != hipSuccess) return hip_fail(err, "zero-copy seal");
+  }
+  if (nblk > nseal) {
+    err = launch_crypt(false, c.keys + nseal, nblk - nseal, src, dst, (uint8_t*)(uintptr_t)c.d_h_ok + nseal, st);
+    if (err != hipSuccess) return hip_fail(err, "zero-copy open");
+  }
+  err = hipEventRecord(c.done, st);
+  if (err != hipSuccess) return hip_fail(err, "zero-copy event");
+  return XS_OK;
+}
+
 // Issue one combined batch on coalescing slot c (asynchronously; completion = c.done).
 static int engine_issue_batch(xs_engine* e, xs_engine::CSlot& c) {
   auto& batch = c.batch;
@@ -552,9 +627,23 @@ static int engine_issue_batch(xs_engine* e, xs_engine::CSlot& c) {
   hipStream_t st = c.s;
   std::vector<uint64_t> blk0(batch.size()), inoff(batch.size()), outoff(batch.size());
   uint64_t nblk = 0, in_pos = 0, out_pos = 0;
+  // zero-copy batch: every request's buffers are pinned; descriptors then hold offsets of the
+  // caller buffers themselves from the lowest input / output address
+  c.zc = true;
+  uint64_t sbase = UINT64_MAX, dbase = UINT64_MAX;
+  for (const auto* q : batch) {
+    c.zc = c.zc && q->zc;
+    sbase = std::min(sbase, q->d_in);
+    dbase = std::min(dbase, q->d_out);
+  }
   for (size_t r = 0; r < batch.size(); r++) {
-    const auto* q = batch[r];
+    auto* q = batch[r];
     blk0[r] = nblk;
+    q->blk0 = nblk;
+    if (c.zc) {
+      in_pos = q->d_in - sbase;
+      out_pos = q->d_out - dbase;
+    }
     inoff[r] = in_pos;
     outoff[r] = out_pos;
     for (uint64_t j = 0; j < q->nblocks; j++) {
@@ -577,6 +666,7 @@ static int engine_issue_batch(xs_engine* e, xs_engine::CSlot& c) {
     in_pos = (in_pos + q->in_len + 15) & ~15ull;
     out_pos = (out_pos + q->out_len + 15) & ~15ull;
   }
+  if (c.zc) return engine_issue_zero_copy(c, blk0, nblk);
   hipError_t err = hipMemcpyAsync(c.desc, c.h_desc, nblk * sizeof(xs_block_desc), hipMemcpyHostToDevice, st);
   for (size_t r = 0; r < batch.size() && err == hipSuccess; r++)
     err = hipMemcpyAsync(c.in + inoff[r], batch[r]->in, batch[r]->in_len, hipMemcpyHostToDevice, st);
@@ -626,6 +716,9 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
   req.ok = ok;
   req.rc = XS_OK;
   req.done = false;
+  req.zc = e->zero_copy && host_dev_ptr(in, &req.d_in) && host_dev_ptr(out, &req.d_out) &&
+           !(req.d_in & 15u) && !(req.d_out & 15u);
+  if (!req.zc) req.d_in = req.d_out = 0;
   std::unique_lock<std::mutex> lk(e->qmu);
   e->queue.push_back(&req);
   while (!req.done) {
@@ -663,6 +756,9 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
       } else {
         (void)hipStreamSynchronize(c.s);
       }
+      if (c.rc == XS_OK && c.zc)
+        for (auto* q : c.batch)
+          if (!q->seal) memcpy(q->ok, c.h_ok + q->blk0, q->nblocks);
       lk.lock();
       for (auto* q : c.batch) {
         q->rc = c.rc;

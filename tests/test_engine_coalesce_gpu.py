@@ -44,7 +44,27 @@ def _seal_expected(plain, nonce0, first, key):
     return b"".join(out)
 
 
-def _run(L, e, nthreads=12, calls=8):
+class _Pinned:
+    """xs_host_alloc'd buffer (page-locked, device-mapped): the engine's zero-copy path."""
+
+    def __init__(self, L, data_or_len):
+        self.L = L
+        n = data_or_len if isinstance(data_or_len, int) else len(data_or_len)
+        self.n = n
+        self.p = L.xs_host_alloc(max(n, 1))
+        assert self.p
+        if not isinstance(data_or_len, int):
+            ctypes.memmove(self.p, bytes(data_or_len), n)
+
+    @property
+    def raw(self):
+        return ctypes.string_at(self.p, self.n)
+
+    def __del__(self):
+        self.L.xs_host_free(self.p)
+
+
+def _run(L, e, nthreads=12, calls=8, pinned=False):
     keys = [splitmix64_bytes(1, 32), splitmix64_bytes(2, 32)]
     errors = []
     start = threading.Barrier(nthreads)
@@ -59,8 +79,12 @@ def _run(L, e, nthreads=12, calls=8):
                 nonce0 = b"\xfe" + b"\xff" * 7 + splitmix64_bytes(t, 16) if i % 3 == 0 else splitmix64_bytes(7 * t + i, 24)
                 first = [0, 1, 255, 1 << 33][i % 4]
                 nb = (n + 65535) // 65536
-                body = ctypes.create_string_buffer(n + 16 * nb)
-                assert L.xs_engine_seal(e, key, nonce0, first, plain, n, body) == 0
+                if pinned:
+                    src, body = _Pinned(L, plain), _Pinned(L, n + 16 * nb)
+                    assert L.xs_engine_seal(e, key, nonce0, first, src.p, n, body.p) == 0
+                else:
+                    body = ctypes.create_string_buffer(n + 16 * nb)
+                    assert L.xs_engine_seal(e, key, nonce0, first, plain, n, body) == 0
                 want = _seal_expected(plain, nonce0, first, key)
                 assert body.raw == want, (t, i, n)
                 wire = bytearray(want)
@@ -68,9 +92,13 @@ def _run(L, e, nthreads=12, calls=8):
                 if i % 2 and nb > 1:
                     wire[65552 + 5] ^= 1  # a tag byte of block 1
                     bad.add(1)
-                out = ctypes.create_string_buffer(n)
                 ok = (ctypes.c_uint8 * nb)()
-                assert L.xs_engine_open(e, key, nonce0, first, bytes(wire), len(wire), out, ok) == 0
+                if pinned:
+                    win, out = _Pinned(L, wire), _Pinned(L, n)
+                    assert L.xs_engine_open(e, key, nonce0, first, win.p, len(wire), out.p, ok) == 0
+                else:
+                    out = ctypes.create_string_buffer(n)
+                    assert L.xs_engine_open(e, key, nonce0, first, bytes(wire), len(wire), out, ok) == 0
                 assert [j for j in range(nb) if not ok[j]] == sorted(bad), (t, i)
                 exp = bytearray(plain)
                 for j in bad:
@@ -105,3 +133,14 @@ def test_uncoalesced_engine_matches_oracle(eng):
     _run(L, e, nthreads=4, calls=6)
     assert _stats(L, e) == before
     L.xs_engine_set_coalesce(e, 1)
+
+
+def test_coalesced_engine_zero_copy_pinned(eng):
+    # pinned caller buffers: combined batches hand the callers' own memory to the kernels
+    # (keygen reads the descriptors from pinned host memory, crypt reads/writes over PCIe)
+    L, e = eng
+    L.xs_engine_set_coalesce(e, 1)
+    b0, r0, _ = _stats(L, e)
+    ncalls = _run(L, e, pinned=True)
+    b1, r1, _ = _stats(L, e)
+    assert r1 - r0 == ncalls and b1 - b0 < r1 - r0
