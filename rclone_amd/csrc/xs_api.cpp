@@ -268,6 +268,9 @@ struct xs_engine {
     uint8_t* d_out = nullptr;
     BlockKey* d_keys = nullptr;
     uint8_t* d_ok = nullptr;
+    uint8_t* zc_keys = nullptr;  // key schedules of a zero-copy chunk (kZcChunk blocks)
+    uint8_t* zc_ok = nullptr;
+    size_t zc_keys_cap = 0, zc_ok_cap = 0;
   };
   std::vector<Slot> slots;
   // ---- cross-caller coalescing (group commit, see engine_submit)
@@ -339,6 +342,8 @@ static bool host_dev_ptr(const void* p, uint64_t* dev) {
   return true;
 }
 
+constexpr uint64_t kZcChunk = 4096;  // blocks per zero-copy launch of a large pinned request
+
 static bool grow(uint8_t** p, size_t* cap, size_t need) {
   if (*cap >= need) return true;
   (void)hipFree(*p);
@@ -358,6 +363,8 @@ static void engine_free(xs_engine* e) {
     (void)hipFree(sl.d_out);
     (void)hipFree(sl.d_keys);
     (void)hipFree(sl.d_ok);
+    (void)hipFree(sl.zc_keys);
+    (void)hipFree(sl.zc_ok);
     if (sl.s) (void)hipStreamDestroy(sl.s);
   }
   for (auto& c : e->cslots) {
@@ -484,6 +491,23 @@ static int engine_seal_direct(xs_engine* e, const uint8_t key[32], const uint8_t
   const KeyArg k = key_arg(key);
   const NonceArg n = nonce_arg(nonce0);
   const uint64_t nblocks = (plain_len + XS_BLOCK_DATA - 1) / XS_BLOCK_DATA;
+  uint64_t dp = 0, db = 0;
+  if (e->zero_copy && host_dev_ptr(plain, &dp) && host_dev_ptr(body, &db) && !(dp & 15u) && !(db & 15u)) {
+    // pinned caller buffers: the kernels read and write them over PCIe in large chunks (the
+    // link, not the launches, is then the limit), no staging copies
+    for (uint64_t b0 = 0, chunk = 0; b0 < nblocks; b0 += kZcChunk, chunk++) {
+      auto& sl = e->slots[chunk % e->slots.size()];
+      const uint64_t nb = std::min<uint64_t>(nblocks - b0, kZcChunk);
+      const uint64_t in_off = b0 * XS_BLOCK_DATA;
+      if (!grow(&sl.zc_keys, &sl.zc_keys_cap, kZcChunk * sizeof(BlockKey))) return hip_fail(hipErrorOutOfMemory, "keys");
+      hipError_t err = launch_keygen(0, k, n, first_block + b0, plain_len - in_off, nb, nullptr, (BlockKey*)sl.zc_keys, sl.s);
+      if (err != hipSuccess) return hip_fail(err, "keygen");
+      err = launch_crypt(true, (BlockKey*)sl.zc_keys, nb, (const uint8_t*)(uintptr_t)(dp + in_off),
+                         (uint8_t*)(uintptr_t)(db + b0 * XS_BLOCK_SIZE), nullptr, sl.s);
+      if (err != hipSuccess) return hip_fail(err, "seal");
+    }
+    return engine_sync(e);
+  }
   for (uint64_t b0 = 0, chunk = 0; b0 < nblocks; b0 += e->batch, chunk++) {
     auto& sl = e->slots[chunk % e->slots.size()];
     const uint64_t nb = (nblocks - b0) < e->batch ? (nblocks - b0) : e->batch;
@@ -526,6 +550,25 @@ static int engine_open_direct(xs_engine* e, const uint8_t key[32], const uint8_t
   if (hipSetDevice(e->device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
   const KeyArg k = key_arg(key);
   const NonceArg n = nonce_arg(nonce0);
+  uint64_t dbody = 0, dplain = 0;
+  if (e->zero_copy && host_dev_ptr(body, &dbody) && host_dev_ptr(plain, &dplain) && !(dbody & 15u) && !(dplain & 15u)) {
+    // pinned caller buffers: no data copies, only the verdicts come back
+    for (uint64_t b0 = 0, chunk = 0; b0 < nblocks; b0 += kZcChunk, chunk++) {
+      auto& sl = e->slots[chunk % e->slots.size()];
+      const uint64_t nb = std::min<uint64_t>(nblocks - b0, kZcChunk);
+      const uint64_t in_off = b0 * XS_BLOCK_SIZE;
+      if (!grow(&sl.zc_keys, &sl.zc_keys_cap, kZcChunk * sizeof(BlockKey)) || !grow(&sl.zc_ok, &sl.zc_ok_cap, kZcChunk))
+        return hip_fail(hipErrorOutOfMemory, "keys");
+      hipError_t err = launch_keygen(1, k, n, first_block + b0, body_len - in_off, nb, nullptr, (BlockKey*)sl.zc_keys, sl.s);
+      if (err != hipSuccess) return hip_fail(err, "keygen");
+      err = launch_crypt(false, (BlockKey*)sl.zc_keys, nb, (const uint8_t*)(uintptr_t)(dbody + in_off),
+                         (uint8_t*)(uintptr_t)(dplain + b0 * XS_BLOCK_DATA), sl.zc_ok, sl.s);
+      if (err != hipSuccess) return hip_fail(err, "open");
+      err = hipMemcpyAsync(ok + b0, sl.zc_ok, nb, hipMemcpyDeviceToHost, sl.s);
+      if (err != hipSuccess) return hip_fail(err, "D2H ok");
+    }
+    return engine_sync(e);
+  }
   for (uint64_t b0 = 0, chunk = 0; b0 < nblocks; b0 += e->batch, chunk++) {
     auto& sl = e->slots[chunk % e->slots.size()];
     const uint64_t nb = (nblocks - b0) < e->batch ? (nblocks - b0) : e->batch;

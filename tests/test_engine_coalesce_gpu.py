@@ -71,7 +71,7 @@ def _run(L, e, nthreads=12, calls=8, pinned=False):
 
     def worker(t):
         try:
-            start.wait()
+            cases = []  # everything but the engine calls is prepared before the start line
             for i in range(calls):
                 key = keys[(t + i) % 2]
                 n = [1, 100, 65536, 65537, 3 * 65536 - 5, 200000][(t * 3 + i) % 6]
@@ -79,31 +79,29 @@ def _run(L, e, nthreads=12, calls=8, pinned=False):
                 nonce0 = b"\xfe" + b"\xff" * 7 + splitmix64_bytes(t, 16) if i % 3 == 0 else splitmix64_bytes(7 * t + i, 24)
                 first = [0, 1, 255, 1 << 33][i % 4]
                 nb = (n + 65535) // 65536
-                if pinned:
-                    src, body = _Pinned(L, plain), _Pinned(L, n + 16 * nb)
-                    assert L.xs_engine_seal(e, key, nonce0, first, src.p, n, body.p) == 0
-                else:
-                    body = ctypes.create_string_buffer(n + 16 * nb)
-                    assert L.xs_engine_seal(e, key, nonce0, first, plain, n, body) == 0
                 want = _seal_expected(plain, nonce0, first, key)
-                assert body.raw == want, (t, i, n)
                 wire = bytearray(want)
                 bad = set()
                 if i % 2 and nb > 1:
                     wire[65552 + 5] ^= 1  # a tag byte of block 1
                     bad.add(1)
-                ok = (ctypes.c_uint8 * nb)()
-                if pinned:
-                    win, out = _Pinned(L, wire), _Pinned(L, n)
-                    assert L.xs_engine_open(e, key, nonce0, first, win.p, len(wire), out.p, ok) == 0
-                else:
-                    out = ctypes.create_string_buffer(n)
-                    assert L.xs_engine_open(e, key, nonce0, first, bytes(wire), len(wire), out, ok) == 0
-                assert [j for j in range(nb) if not ok[j]] == sorted(bad), (t, i)
                 exp = bytearray(plain)
                 for j in bad:
                     exp[j * 65536:(j + 1) * 65536] = bytes(len(exp[j * 65536:(j + 1) * 65536]))
-                assert out.raw == bytes(exp), (t, i)
+                if pinned:
+                    bufs = (_Pinned(L, plain), _Pinned(L, n + 16 * nb), _Pinned(L, wire), _Pinned(L, n))
+                else:
+                    bufs = (plain, ctypes.create_string_buffer(n + 16 * nb), bytes(wire), ctypes.create_string_buffer(n))
+                cases.append((key, n, nonce0, first, nb, want, bad, bytes(exp), bufs))
+            ptr = (lambda b: b.p) if pinned else (lambda b: b)
+            start.wait()
+            for i, (key, n, nonce0, first, nb, want, bad, exp, (src, body, win, out)) in enumerate(cases):
+                assert L.xs_engine_seal(e, key, nonce0, first, ptr(src), n, ptr(body)) == 0
+                assert body.raw == want, (t, i, n)
+                ok = (ctypes.c_uint8 * nb)()
+                assert L.xs_engine_open(e, key, nonce0, first, ptr(win), len(want), ptr(out), ok) == 0
+                assert [j for j in range(nb) if not ok[j]] == sorted(bad), (t, i)
+                assert out.raw == exp, (t, i)
         except BaseException as ex:  # noqa: BLE001
             errors.append((t, repr(ex)))
 
@@ -144,3 +142,29 @@ def test_coalesced_engine_zero_copy_pinned(eng):
     ncalls = _run(L, e, pinned=True)
     b1, r1, _ = _stats(L, e)
     assert r1 - r0 == ncalls and b1 - b0 < r1 - r0
+
+
+def test_direct_zero_copy_large_pinned(eng):
+    # a pinned request larger than a combined batch: chunked keygen + crypt straight on the
+    # caller's host memory (no staging copies), verdicts copied back per chunk
+    L, e = eng
+    key = splitmix64_bytes(3, 32)
+    nonce0 = b"\xf0" + b"\xff" * 7 + splitmix64_bytes(4, 16)
+    n = 150 * 65536 + 4321
+    nb = (n + 65535) // 65536
+    plain = splitmix64_bytes(5, n)
+    src, body = _Pinned(L, plain), _Pinned(L, n + 16 * nb)
+    assert L.xs_engine_seal(e, key, nonce0, 7, src.p, n, body.p) == 0
+    want = _seal_expected(plain, nonce0, 7, key)
+    assert body.raw == want
+    wire = bytearray(want)
+    wire[65552 * 70 + 16 + 100] ^= 0x10   # ciphertext byte of block 70
+    wire[65552 * (nb - 1) + 3] ^= 0x01    # tag byte of the last (partial) block
+    win, out = _Pinned(L, wire), _Pinned(L, n)
+    ok = (ctypes.c_uint8 * nb)()
+    assert L.xs_engine_open(e, key, nonce0, 7, win.p, len(wire), out.p, ok) == 0
+    assert [j for j in range(nb) if not ok[j]] == [70, nb - 1]
+    exp = bytearray(plain)
+    for j in (70, nb - 1):
+        exp[j * 65536:(j + 1) * 65536] = bytes(len(exp[j * 65536:(j + 1) * 65536]))
+    assert out.raw == bytes(exp)
