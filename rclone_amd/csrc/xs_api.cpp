@@ -325,7 +325,7 @@ struct xs_engine {
 
 // Device address of pinned (page-locked, device-mapped) host memory, or false for anything else
 // (pageable memory, device memory): only such buffers are handed to the kernels directly.
-static bool host_dev_ptr(const void* p, uint64_t* dev) {
+static bool host_dev_ptr(const void* p, uint64_t* dev, int device) {
   if (!p) return false;
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -333,6 +333,8 @@ static bool host_dev_ptr(const void* p, uint64_t* dev) {
     return false;
   }
   if (a.type != hipMemoryTypeHost) return false;
+  // mapped for this engine's device: allocated portable, or while that device was current
+  if (!(a.allocationFlags & hipHostMallocPortable) && a.device != device) return false;
   void* d = nullptr;
   if (hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess || !d) {
     (void)hipGetLastError();
@@ -429,7 +431,7 @@ extern "C" xs_engine* xs_engine_create(int device, uint32_t batch_blocks, int ns
         hipMalloc(&c.keys, (size_t)batch_blocks * sizeof(BlockKey)) != hipSuccess ||
         hipHostMalloc(&c.h_desc, (size_t)batch_blocks * sizeof(xs_block_desc), hipHostMallocPortable) != hipSuccess ||
         hipHostMalloc(&c.h_ok, batch_blocks, hipHostMallocPortable) != hipSuccess ||
-        !host_dev_ptr(c.h_desc, &c.d_h_desc) || !host_dev_ptr(c.h_ok, &c.d_h_ok)) {
+        !host_dev_ptr(c.h_desc, &c.d_h_desc, device) || !host_dev_ptr(c.h_ok, &c.d_h_ok, device)) {
       set_error("xs_engine_create: device allocation failed");
       engine_free(e);
       return nullptr;
@@ -492,7 +494,7 @@ static int engine_seal_direct(xs_engine* e, const uint8_t key[32], const uint8_t
   const NonceArg n = nonce_arg(nonce0);
   const uint64_t nblocks = (plain_len + XS_BLOCK_DATA - 1) / XS_BLOCK_DATA;
   uint64_t dp = 0, db = 0;
-  if (e->zero_copy && host_dev_ptr(plain, &dp) && host_dev_ptr(body, &db) && !(dp & 15u) && !(db & 15u)) {
+  if (e->zero_copy && host_dev_ptr(plain, &dp, e->device) && host_dev_ptr(body, &db, e->device) && !(dp & 15u) && !(db & 15u)) {
     // pinned caller buffers: the kernels read and write them over PCIe in large chunks (the
     // link, not the launches, is then the limit), no staging copies
     for (uint64_t b0 = 0, chunk = 0; b0 < nblocks; b0 += kZcChunk, chunk++) {
@@ -551,7 +553,7 @@ static int engine_open_direct(xs_engine* e, const uint8_t key[32], const uint8_t
   const KeyArg k = key_arg(key);
   const NonceArg n = nonce_arg(nonce0);
   uint64_t dbody = 0, dplain = 0;
-  if (e->zero_copy && host_dev_ptr(body, &dbody) && host_dev_ptr(plain, &dplain) && !(dbody & 15u) && !(dplain & 15u)) {
+  if (e->zero_copy && host_dev_ptr(body, &dbody, e->device) && host_dev_ptr(plain, &dplain, e->device) && !(dbody & 15u) && !(dplain & 15u)) {
     // pinned caller buffers: no data copies, only the verdicts come back
     for (uint64_t b0 = 0, chunk = 0; b0 < nblocks; b0 += kZcChunk, chunk++) {
       auto& sl = e->slots[chunk % e->slots.size()];
@@ -759,7 +761,7 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
   req.ok = ok;
   req.rc = XS_OK;
   req.done = false;
-  req.zc = e->zero_copy && host_dev_ptr(in, &req.d_in) && host_dev_ptr(out, &req.d_out) &&
+  req.zc = e->zero_copy && host_dev_ptr(in, &req.d_in, e->device) && host_dev_ptr(out, &req.d_out, e->device) &&
            !(req.d_in & 15u) && !(req.d_out & 15u);
   if (!req.zc) req.d_in = req.d_out = 0;
   std::unique_lock<std::mutex> lk(e->qmu);
