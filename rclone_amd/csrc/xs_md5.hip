@@ -143,14 +143,37 @@ __global__ void __launch_bounds__(64) xs_md5(const xs_md5_desc* __restrict__ des
     const uint64_t total = plen + len;
     const uint64_t nfull = total >> 6;
     uint32_t m[16];
-#pragma unroll 1
-    for (uint64_t b = 0; b < nfull; b++) {
+    // Full blocks, loads two blocks ahead of the compression (one lane's stream is a serial
+    // chain: without the prefetch every block waited a whole HBM round trip).  Block 0 holds
+    // the prefix; from block 1 on the stream is plain data at body + 64 b - prefix_len.
+    const uint8_t* body = src + off - plen;
+    uint4 A[4], B[4], C[4];
+    auto fetch = [&](uint4 (&q)[4], uint64_t b) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) q[j] = *reinterpret_cast<const uint4*>(body + 64u * b + 16u * j);
+    };
+    auto compress = [&](const uint4 (&q)[4]) {
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        const uint4 v = chunk(prefix, plen, off, src, 4 * b + j);
-        m[4 * j] = v.x; m[4 * j + 1] = v.y; m[4 * j + 2] = v.z; m[4 * j + 3] = v.w;
+        m[4 * j] = q[j].x; m[4 * j + 1] = q[j].y; m[4 * j + 2] = q[j].z; m[4 * j + 3] = q[j].w;
       }
       md5_block(st, m);
+    };
+    if (nfull > 0) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) A[j] = chunk(prefix, plen, off, src, j);
+    }
+    if (nfull > 1) fetch(B, 1);
+#pragma unroll 1
+    for (uint64_t b = 0; b < nfull; b += 3) {  // A, B, C rotate: no register moves, no early waits
+      if (b + 2 < nfull) fetch(C, b + 2);
+      compress(A);
+      if (b + 1 >= nfull) break;
+      if (b + 3 < nfull) fetch(A, b + 3);
+      compress(B);
+      if (b + 2 >= nfull) break;
+      if (b + 4 < nfull) fetch(B, b + 4);
+      compress(C);
     }
     // tail: remaining bytes, 0x80, zero pad, 64-bit little-endian bit length
     const uint32_t rem = (uint32_t)(total & 63u);
