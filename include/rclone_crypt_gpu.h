@@ -255,6 +255,85 @@ void rc_decrypter_free(rc_decrypter *d);
 int32_t rc_hash_batch_with_nonce(rc_cipher *c, uint64_t n, const rc_reader *srcs, const uint8_t *nonces,
                                  uint8_t *md5, int32_t *errs);
 
+/* ------------------------------------------------------------------------------------
+ * File-name cipher (cipher.go:120-618): NameEncryptionMode, fileNameEncoding, encryptSegment /
+ * decryptSegment (EME-AES-256 over pkcs7-padded names, github.com/rfjakob/eme v1.2.0, run on
+ * the GPU by xs_eme_batch_dev), obfuscateSegment / deobfuscateSegment, Encrypt/DecryptFileName,
+ * Encrypt/DecryptDirName, with lib/version handling and the encrypted suffix of mode "off".
+ * ---------------------------------------------------------------------------------- */
+#define RC_NAME_OFF 0        /* NameEncryptionOff (cipher.go:87) */
+#define RC_NAME_STANDARD 1   /* NameEncryptionStandard */
+#define RC_NAME_OBFUSCATE 2  /* NameEncryptionObfuscated */
+#define RC_ENC_BASE32 0      /* caseInsensitiveBase32Encoding (cipher.go:127-152) */
+#define RC_ENC_BASE64 1      /* base64.RawURLEncoding */
+#define RC_ENC_BASE32768 2   /* base32768.SafeEncoding (github.com/Max-Sum/base32768) */
+
+#define RC_ERR_NOT_A_MULTIPLE_OF_BLOCKSIZE (-130) /* ErrorNotAMultipleOfBlocksize */
+#define RC_ERR_TOO_SHORT_AFTER_DECODE (-131)      /* ErrorTooShortAfterDecode */
+#define RC_ERR_TOO_LONG_AFTER_DECODE (-132)       /* ErrorTooLongAfterDecode */
+#define RC_ERR_BAD_BASE32_ENCODING (-133)         /* ErrorBadBase32Encoding */
+#define RC_ERR_NOT_AN_ENCRYPTED_FILE (-134)       /* ErrorNotAnEncryptedFile */
+#define RC_ERR_PKCS7_NOT_FOUND (-140)             /* pkcs7.ErrorPaddingNotFound (pkcs7.go:10) */
+#define RC_ERR_PKCS7_NOT_A_MULTIPLE (-141)        /* pkcs7.ErrorPaddingNotAMultiple */
+#define RC_ERR_PKCS7_TOO_LONG (-142)              /* pkcs7.ErrorPaddingTooLong */
+#define RC_ERR_PKCS7_TOO_SHORT (-143)             /* pkcs7.ErrorPaddingTooShort */
+#define RC_ERR_PKCS7_NOT_ALL_THE_SAME (-144)      /* pkcs7.ErrorPaddingNotAllTheSame */
+#define RC_ERR_BASE32_CORRUPT (-150)    /* base32.CorruptInputError(arg) */
+#define RC_ERR_BASE64_CORRUPT (-151)    /* base64.CorruptInputError(arg) */
+#define RC_ERR_BASE32768_CORRUPT (-152) /* base32768.CorruptInputError(arg) */
+#define RC_ERR_UNKNOWN_MODE (-153)      /* "unknown file name encryption mode %q" (cipher.go:101) */
+#define RC_ERR_UNKNOWN_ENCODING (-154)  /* "unknown file name encoding mode %q" (cipher.go:166) */
+#define RC_ERR_NAME_TOO_LONG (-155)     /* padded name > 2048 bytes: eme.Transform panics there */
+
+/* One name for xs_eme_batch_dev: nblk 16-byte blocks (1..128) at byte offset off (16-aligned). */
+typedef struct xs_name_desc {
+  uint64_t off;
+  uint32_t nblk;
+  uint32_t reserved;
+} xs_name_desc;
+
+/* eme.Transform(aes.NewCipher(name_key), tweak, names, direction) for every descriptor, on the
+ * GPU: encrypt != 0 -> DirectionEncrypt.  d_src and d_dst are device buffers of buf_len bytes
+ * (they may be the same buffer: in place); each name is read at d_src+off and written at
+ * d_dst+off.  A descriptor out of range is skipped (its output is unspecified). */
+int xs_eme_batch_dev(int encrypt, const uint8_t name_key[32], const uint8_t tweak[16], const xs_name_desc *d_desc,
+                     uint64_t n, const void *d_src, void *d_dst, uint64_t buf_len, void *stream);
+
+/* NewNameEncryptionMode / NewNameEncoding (cipher.go:92, :155): parse a config string. */
+int32_t rc_new_name_encryption_mode(const char *s, int32_t *mode);
+int32_t rc_new_name_encoding(const char *s, int32_t *enc);
+/* newCipher's name arguments (cipher.go:187): mode, dirNameEncrypt, enc; setEncryptedSuffix :207. */
+void rc_cipher_set_name_encryption(rc_cipher *c, int32_t mode, int32_t dir_name_encrypt, int32_t enc);
+void rc_cipher_set_encrypted_suffix(rc_cipher *c, const char *suffix);
+
+/* fileNameEncoding.EncodeToString / DecodeString for one encoding.  Encode writes at most
+ * cap bytes and returns the full encoded length; decode returns RC_NIL or an RC_ERR_* value
+ * with *err_arg = the CorruptInputError offset. */
+int64_t rc_name_encode(int32_t enc, const uint8_t *src, uint64_t n, char *out, uint64_t cap);
+int32_t rc_name_decode(int32_t enc, const char *s, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *out_len,
+                       int64_t *err_arg);
+
+/* Batched name operations: one GPU EME launch for every segment of every name in the batch.
+ * op: which cipher.go function is applied to each input string. */
+#define RC_OP_ENCRYPT_FILE_NAME 0 /* EncryptFileName :542 */
+#define RC_OP_DECRYPT_FILE_NAME 1 /* DecryptFileName :600 */
+#define RC_OP_ENCRYPT_DIR_NAME 2  /* EncryptDirName :550 */
+#define RC_OP_DECRYPT_DIR_NAME 3  /* DecryptDirName :613 */
+#define RC_OP_ENCRYPT_SEGMENT 4   /* encryptSegment :280 (standard mode) */
+#define RC_OP_DECRYPT_SEGMENT 5   /* decryptSegment :293 (standard mode) */
+#define RC_OP_OBFUSCATE_SEGMENT 6 /* obfuscateSegment :315 */
+#define RC_OP_DEOBFUSCATE_SEGMENT 7 /* deobfuscateSegment :402 */
+typedef struct rc_names rc_names;
+/* Runs op over n strings (in[i], in_len[i] bytes).  Returns RC_NIL and *out, or RC_ERR_GPU /
+ * RC_ERR_INVALID (no result).  Per-name errors are in the result, as the reference returns them. */
+int32_t rc_names_run(rc_cipher *c, int32_t op, uint64_t n, const char *const *in, const uint64_t *in_len,
+                     rc_names **out);
+/* Result i: string (not NUL-terminated), its length, error value and error argument. */
+void rc_names_get(const rc_names *r, uint64_t i, const char **s, uint64_t *len, int32_t *err, int64_t *err_arg);
+/* Device time of the batch's EME kernel (ms, HIP events), 0 when no segment went to the GPU. */
+double rc_names_kernel_ms(const rc_names *r);
+void rc_names_free(rc_names *r);
+
 /* Message of an rc_* error value (the reference's error string). */
 const char *rc_error_string(int32_t err);
 

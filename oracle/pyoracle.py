@@ -1,7 +1,7 @@
 """TEST INFRASTRUCTURE ONLY -- ctypes front-end for oracle/build/liboracle.so.
 
 The checker for the HIP path (never the thing measured as the product, never shipped).
-Built from oracle/xsalsa_oracle.c by oracle/Makefile (see that file's header for the
+Built from oracle/xsalsa_oracle.c and oracle/eme_oracle.c by oracle/Makefile (see that file's header for the
 reference file:line each function restates).
 """
 import ctypes
@@ -50,6 +50,12 @@ def _load():
     lib.orc_seal_desc.restype = ctypes.c_int
     lib.orc_open_desc.argtypes = [vp, vp, vp, vp, ctypes.c_int64, c_p]
     lib.orc_open_desc.restype = ctypes.c_int
+    # eme_oracle.c (file names)
+    lib.orc_aes256_expand.argtypes = [c_p, vp]
+    lib.orc_aes256_encrypt.argtypes = [vp, c_p, vp]
+    lib.orc_aes256_decrypt.argtypes = [vp, c_p, vp]
+    lib.orc_eme_transform.argtypes = [c_p, c_p, c_p, vp, ctypes.c_int, ctypes.c_int]
+    lib.orc_eme_transform.restype = ctypes.c_int
     return lib
 
 
@@ -133,3 +139,52 @@ def open_desc(dst, ok, src, desc, key: bytes) -> int:
     assert desc.dtype.itemsize == 48
     return lib().orc_open_desc(dst.ctypes.data, ok.ctypes.data, src.ctypes.data, desc.ctypes.data, len(desc),
                                bytes(key))
+
+
+# ------------------------------------------------------------------ file names (eme_oracle.c)
+def aes256_encrypt(key: bytes, block: bytes) -> bytes:
+    rk = ctypes.create_string_buffer(240)
+    lib().orc_aes256_expand(bytes(key), rk)
+    out = ctypes.create_string_buffer(16)
+    lib().orc_aes256_encrypt(rk, bytes(block), out)
+    return out.raw
+
+
+def aes256_decrypt(key: bytes, block: bytes) -> bytes:
+    rk = ctypes.create_string_buffer(240)
+    lib().orc_aes256_expand(bytes(key), rk)
+    out = ctypes.create_string_buffer(16)
+    lib().orc_aes256_decrypt(rk, bytes(block), out)
+    return out.raw
+
+
+def eme_transform(key: bytes, tweak: bytes, data: bytes, encrypt: bool) -> bytes:
+    """eme.Transform(aes(key), tweak, data, direction) (rfjakob/eme v1.2.0)."""
+    data = bytes(data)
+    assert len(data) % 16 == 0
+    out = ctypes.create_string_buffer(max(len(data), 1))
+    rc = lib().orc_eme_transform(bytes(key), bytes(tweak), data, out, len(data) // 16, 0 if encrypt else 1)
+    if rc != 0:
+        raise ValueError("EME operates on 1 to 128 block-cipher blocks")
+    return out.raw[:len(data)]
+
+
+def pkcs7_pad(b: bytes) -> bytes:
+    p = 16 - len(b) % 16
+    return bytes(b) + bytes([p]) * p
+
+
+def pkcs7_unpad(b: bytes):
+    """Returns the unpadded bytes or the pkcs7.go error name."""
+    if not b:
+        return "ErrorPaddingNotFound"
+    if len(b) % 16:
+        return "ErrorPaddingNotAMultiple"
+    p = b[-1]
+    if p > 16:
+        return "ErrorPaddingTooLong"
+    if p == 0:
+        return "ErrorPaddingTooShort"
+    if any(x != p for x in b[-p:]):
+        return "ErrorPaddingNotAllTheSame"
+    return b[:-p]

@@ -23,6 +23,13 @@ class XsBlockDesc(ctypes.Structure):
 
 assert ctypes.sizeof(XsBlockDesc) == 48
 
+
+class XsNameDesc(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_uint64), ("nblk", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(XsNameDesc) == 16
+
 READ_FN = ctypes.CFUNCTYPE(i64, vp, c_u8p, i64, ctypes.POINTER(i32))
 CLOSE_FN = ctypes.CFUNCTYPE(i32, vp)
 RANGE_SEEK_FN = ctypes.CFUNCTYPE(i32, vp, i64, i32, i64)
@@ -88,6 +95,19 @@ _SIGS = [
     ("rc_decrypter_free", None, [vp]),
     ("rc_hash_batch_with_nonce", i32, [vp, u64, vp, vp, vp, vp]),
     ("rc_error_string", ctypes.c_char_p, [i32]),
+    # file names (cipher.go:120-618)
+    ("xs_eme_batch_dev", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, vp, u64, vp, vp, u64, vp]),
+    ("rc_new_name_encryption_mode", i32, [ctypes.c_char_p, ctypes.POINTER(i32)]),
+    ("rc_new_name_encoding", i32, [ctypes.c_char_p, ctypes.POINTER(i32)]),
+    ("rc_cipher_set_name_encryption", None, [vp, i32, i32, i32]),
+    ("rc_cipher_set_encrypted_suffix", None, [vp, ctypes.c_char_p]),
+    ("rc_name_encode", i64, [i32, ctypes.c_char_p, u64, vp, u64]),
+    ("rc_name_decode", i32, [i32, ctypes.c_char_p, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(i64)]),
+    ("rc_names_run", i32, [vp, i32, u64, vp, vp, ctypes.POINTER(vp)]),
+    ("rc_names_get", None, [vp, u64, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(u64), ctypes.POINTER(i32),
+                            ctypes.POINTER(i64)]),
+    ("rc_names_kernel_ms", ctypes.c_double, [vp]),
+    ("rc_names_free", None, [vp]),
 ]
 
 SYMBOLS = [s[0] for s in _SIGS]

@@ -28,6 +28,7 @@ import ctypes
 import threading
 
 from . import _lib
+from .names import NAME_ENCRYPTION_STANDARD, NameCipherMixin
 
 BLOCK_DATA_SIZE = 65536  # blockDataSize cipher.go:39
 BLOCK_HEADER_SIZE = 16   # blockHeaderSize cipher.go:38
@@ -130,6 +131,11 @@ def _raise(code, wrapped=None):
     raise _ERRS.exc(code, wrapped)
 
 
+def new_cipher(mode, password, salt, dir_name_encrypt, enc):
+    """newCipher (cipher.go:187) with the reference's argument order."""
+    return Cipher(password, salt, mode=mode, dir_name_encrypt=dir_name_encrypt, enc=enc)
+
+
 # ------------------------------------------------------------------ reader adaptation
 class _ReaderBridge:
     """Wraps a Python reader as an rc_reader (io.Reader [+ io.Closer] [+ fs.RangeSeeker])."""
@@ -211,13 +217,16 @@ def decrypted_size(size: int) -> int:
     return v
 
 
-class Cipher:
-    """The crypt data cipher (cipher.go:172 Cipher, :187 newCipher, :231 Key)."""
+class Cipher(NameCipherMixin):
+    """The crypt cipher (cipher.go:172 Cipher, :187 newCipher, :231 Key): data path here, the
+    file-name methods from names.NameCipherMixin."""
 
-    def __init__(self, password: str = "", salt: str = "", pass_bad_blocks: bool = False, batch_blocks: int = 64):
+    def __init__(self, password: str = "", salt: str = "", pass_bad_blocks: bool = False, batch_blocks: int = 64,
+                 mode: int = NAME_ENCRYPTION_STANDARD, dir_name_encrypt: bool = True, enc=None):
         e = ctypes.c_int32(0)
         self._h = _lib.lib().rc_cipher_new(password.encode(), salt.encode(), ctypes.byref(e))
         _raise(e.value)
+        self.set_name_encryption(mode, dir_name_encrypt, enc)
         self._rand = None
         self._rand_bridge = None
         self.pass_bad_blocks = pass_bad_blocks

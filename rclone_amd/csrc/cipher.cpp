@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../../include/rclone_crypt_gpu.h"
+#include "rc_internal.h"
 
 namespace rc {
 bool scrypt(const uint8_t* pw, size_t pwlen, const uint8_t* salt, size_t slen, uint64_t N, int r, int p,
@@ -149,17 +150,7 @@ struct PinnedBuf {
 
 }  // namespace
 
-// ---------------------------------------------------------------- Cipher
-struct rc_cipher {
-  uint8_t data_key[32] = {0};
-  uint8_t name_key[32] = {0};
-  uint8_t name_tweak[16] = {0};
-  bool pass_bad_blocks = false;
-  rc_reader rand{};  // c.cryptoRand; read == NULL -> OS random
-  uint32_t batch_blocks = 64;
-  std::mutex rand_mu;
-};
-
+// ---------------------------------------------------------------- Cipher (struct in rc_internal.h)
 extern "C" int32_t rc_cipher_key(rc_cipher* c, const char* password, const char* salt) {
   if (!c) return RC_ERR_INVALID;
   uint8_t key[80] = {0};
@@ -176,6 +167,7 @@ extern "C" int32_t rc_cipher_key(rc_cipher* c, const char* password, const char*
   memcpy(c->data_key, key, 32);
   memcpy(c->name_key, key + 32, 32);
   memcpy(c->name_tweak, key + 64, 16);
+  xs::aes::expand_key(c->name_key, c->name_tweak, &c->eme);  // aes.NewCipher(c.nameKey[:]) :249
   return RC_NIL;
 }
 
@@ -287,6 +279,22 @@ extern "C" const char* rc_error_string(int32_t e) {
     case RC_ERR_REOPEN: return "couldn't reopen file with offset and limit";
     case RC_ERR_GPU: return "GPU crypt engine failure";
     case RC_ERR_INVALID: return "invalid argument";
+    case RC_ERR_NOT_A_MULTIPLE_OF_BLOCKSIZE: return "not a multiple of blocksize";
+    case RC_ERR_TOO_SHORT_AFTER_DECODE: return "too short after base32 decode";
+    case RC_ERR_TOO_LONG_AFTER_DECODE: return "too long after base32 decode";
+    case RC_ERR_BAD_BASE32_ENCODING: return "bad base32 filename encoding";
+    case RC_ERR_NOT_AN_ENCRYPTED_FILE: return "not an encrypted file - does not match suffix";
+    case RC_ERR_PKCS7_NOT_FOUND: return "bad PKCS#7 padding - not padded";
+    case RC_ERR_PKCS7_NOT_A_MULTIPLE: return "bad PKCS#7 padding - not a multiple of blocksize";
+    case RC_ERR_PKCS7_TOO_LONG: return "bad PKCS#7 padding - too long";
+    case RC_ERR_PKCS7_TOO_SHORT: return "bad PKCS#7 padding - too short";
+    case RC_ERR_PKCS7_NOT_ALL_THE_SAME: return "bad PKCS#7 padding - not all the same";
+    case RC_ERR_BASE32_CORRUPT: return "illegal base32 data at input byte";
+    case RC_ERR_BASE64_CORRUPT: return "illegal base64 data at input byte";
+    case RC_ERR_BASE32768_CORRUPT: return "illegal base32768 data at input byte";
+    case RC_ERR_UNKNOWN_MODE: return "unknown file name encryption mode";
+    case RC_ERR_UNKNOWN_ENCODING: return "unknown file name encoding mode";
+    case RC_ERR_NAME_TOO_LONG: return "EME operates on 1 to 128 block-cipher blocks";
     default: return "reader error";
   }
 }

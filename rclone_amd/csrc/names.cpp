@@ -1,0 +1,972 @@
+// names.cpp -- host mirror of the file-name half of rclone's backend/crypt/cipher.go (v1.76.0)
+// behind the rc_* C ABI, with the EME-AES-256 segment cipher on the GPU (xs_eme.hip).
+//
+//   NewNameEncryptionMode / String        cipher.go:92-118   rc_new_name_encryption_mode
+//   caseInsensitiveBase32Encoding         cipher.go:127-152  enc_base32 / dec_base32
+//   NewNameEncoding (base64, base32768)   cipher.go:155-169  rc_new_name_encoding
+//   encryptSegment / decryptSegment       cipher.go:264-312  batched: host pkcs7 + encoding,
+//                                                            one GPU EME launch per batch
+//   obfuscateSegment / deobfuscateSegment cipher.go:315-479  obfuscate / deobfuscate
+//   encryptFileName / EncryptFileName / EncryptDirName / decryptFileName / DecryptFileName /
+//   DecryptDirName                        cipher.go:482-618  run_path
+//   lib/version Match / Remove / Add      lib/version/version.go
+//   pkcs7 Pad / Unpad                     backend/crypt/pkcs7/pkcs7.go:20-63
+//
+// The reference encrypts one path segment per call; here a batch of names (a directory
+// listing, a sync's worth of object names) is split into segments on the host, every segment
+// that needs the block cipher is packed into one pinned buffer and transformed by a single
+// kernel launch, then the results are encoded and reassembled.  Outputs and errors (values
+// and which segment's error wins) are the reference's.
+#include <hip/hip_runtime.h>
+
+#include <cctype>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rc_internal.h"
+#include "xs_internal.h"
+
+namespace xs {
+hipError_t launch_eme(bool encrypt, const aes::EmeKey& key, const xs_name_desc* desc, uint64_t n, const uint8_t* src,
+                      uint8_t* dst, uint64_t buf_len, hipStream_t stream);
+}
+
+namespace {
+
+constexpr int kNameBlock = 16;         // nameCipherBlockSize = aes.BlockSize (cipher.go:33)
+constexpr size_t kMaxCipherName = 2048;  // decryptSegment's limit (cipher.go:303); EME's 128 blocks
+
+// ------------------------------------------------------------------ UTF-8 (Go unicode/utf8)
+constexpr int32_t kRuneError = 0xFFFD;
+
+// utf8.DecodeRuneInString: (RuneError, 1) for an invalid or short sequence.
+int32_t decode_rune(const uint8_t* s, size_t n, size_t* size) {
+  uint8_t b0 = s[0];
+  if (b0 < 0x80) {
+    *size = 1;
+    return b0;
+  }
+  *size = 1;
+  int need;
+  int32_t r;
+  uint8_t lo = 0x80, hi = 0xBF;
+  if (b0 >= 0xC2 && b0 <= 0xDF) {
+    need = 1;
+    r = b0 & 0x1F;
+  } else if (b0 >= 0xE0 && b0 <= 0xEF) {
+    need = 2;
+    r = b0 & 0x0F;
+    if (b0 == 0xE0) lo = 0xA0;
+    if (b0 == 0xED) hi = 0x9F;
+  } else if (b0 >= 0xF0 && b0 <= 0xF4) {
+    need = 3;
+    r = b0 & 0x07;
+    if (b0 == 0xF0) lo = 0x90;
+    if (b0 == 0xF4) hi = 0x8F;
+  } else {
+    return kRuneError;
+  }
+  if (n < (size_t)need + 1) return kRuneError;
+  for (int i = 1; i <= need; i++) {
+    uint8_t b = s[i];
+    if (i == 1 ? (b < lo || b > hi) : (b < 0x80 || b > 0xBF)) return kRuneError;
+    r = (r << 6) | (b & 0x3F);
+  }
+  *size = need + 1;
+  return r;
+}
+
+bool valid_utf8(const std::string& s) {
+  const uint8_t* p = (const uint8_t*)s.data();
+  size_t i = 0;
+  while (i < s.size()) {
+    size_t sz;
+    int32_t r = decode_rune(p + i, s.size() - i, &sz);
+    if (r == kRuneError && sz == 1) return false;
+    i += sz;
+  }
+  return true;
+}
+
+bool valid_rune(int64_t r) { return (r >= 0 && r < 0xD800) || (r > 0xDFFF && r <= 0x10FFFF); }
+
+// strings.Builder.WriteRune: invalid runes are written as U+FFFD.
+void put_rune(std::string& o, int64_t r) {
+  if (!valid_rune(r)) r = kRuneError;
+  if (r < 0x80) {
+    o += (char)r;
+  } else if (r < 0x800) {
+    o += (char)(0xC0 | (r >> 6));
+    o += (char)(0x80 | (r & 0x3F));
+  } else if (r < 0x10000) {
+    o += (char)(0xE0 | (r >> 12));
+    o += (char)(0x80 | ((r >> 6) & 0x3F));
+    o += (char)(0x80 | (r & 0x3F));
+  } else {
+    o += (char)(0xF0 | (r >> 18));
+    o += (char)(0x80 | ((r >> 12) & 0x3F));
+    o += (char)(0x80 | ((r >> 6) & 0x3F));
+    o += (char)(0x80 | (r & 0x3F));
+  }
+}
+
+template <class F>
+void for_runes(const std::string& s, F f) {
+  const uint8_t* p = (const uint8_t*)s.data();
+  size_t i = 0;
+  while (i < s.size()) {
+    size_t sz;
+    int32_t r = decode_rune(p + i, s.size() - i, &sz);
+    f(r);
+    i += sz;
+  }
+}
+
+// ------------------------------------------------------------------ encodings
+struct Err {
+  int32_t code = RC_NIL;
+  int64_t arg = 0;
+};
+
+const char kB32Hex[] = "0123456789ABCDEFGHIJKLMNOPQRSTUV";
+const char kB64Url[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
+
+// base32.HexEncoding.EncodeToString, '=' trimmed, lower-cased (cipher.go:136-140).
+std::string enc_base32(const uint8_t* p, size_t n) {
+  std::string o;
+  o.reserve((n * 8 + 4) / 5);
+  uint64_t acc = 0;
+  int bits = 0;
+  for (size_t i = 0; i < n; i++) {
+    acc = (acc << 8) | p[i];
+    bits += 8;
+    while (bits >= 5) {
+      bits -= 5;
+      o += (char)tolower(kB32Hex[(acc >> bits) & 31]);
+    }
+  }
+  if (bits) o += (char)tolower(kB32Hex[(acc << (5 - bits)) & 31]);
+  return o;
+}
+
+// caseInsensitiveBase32Encoding.DecodeString (cipher.go:143-152) over encoding/base32's
+// decoder: '=' suffix rejected, padding re-added, upper-cased, newlines stripped, then the
+// quantum decoder with Go's CorruptInputError offsets.
+Err dec_base32(const std::string& s0, std::vector<uint8_t>& out) {
+  out.clear();
+  if (!s0.empty() && s0.back() == '=') return {RC_ERR_BAD_BASE32_ENCODING, 0};
+  size_t equals = ((s0.size() + 7) & ~(size_t)7) - s0.size();
+  std::string s;
+  s.reserve(s0.size() + equals);
+  for (char ch : s0) {
+    if (ch == '\r' || ch == '\n') continue;  // stripNewlines
+    s += (ch >= 'a' && ch <= 'z') ? (char)(ch - 32) : ch;
+  }
+  s.append(equals, '=');
+  static int8_t map[256];
+  static bool init = false;
+  if (!init) {
+    memset(map, -1, sizeof map);
+    for (int i = 0; i < 32; i++) map[(uint8_t)kB32Hex[i]] = (int8_t)i;
+    init = true;
+  }
+  const int64_t olen = (int64_t)s.size();
+  size_t pos = 0;
+  bool end = false;
+  while (pos < s.size() && !end) {
+    uint8_t d[8] = {0};
+    int dlen = 8;
+    int j = 0;
+    while (j < 8) {
+      int64_t rem = (int64_t)s.size() - (int64_t)pos;
+      if (rem == 0) return {RC_ERR_BASE32_CORRUPT, olen - rem - j};
+      uint8_t in = (uint8_t)s[pos++];
+      rem--;
+      if (in == '=' && j >= 2 && rem < 8) {
+        if (rem + j < 8 - 1) return {RC_ERR_BASE32_CORRUPT, olen};
+        for (int k = 0; k < 8 - 1 - j; k++)
+          if (rem > k && s[pos + k] != '=') return {RC_ERR_BASE32_CORRUPT, olen - rem + k - 1};
+        dlen = j;
+        end = true;
+        if (dlen == 1 || dlen == 3 || dlen == 6) return {RC_ERR_BASE32_CORRUPT, olen - rem - 1};
+        break;
+      }
+      int8_t v = map[in];
+      if (v < 0) return {RC_ERR_BASE32_CORRUPT, olen - rem - 1};
+      d[j++] = (uint8_t)v;
+    }
+    uint8_t b[5] = {(uint8_t)(d[0] << 3 | d[1] >> 2), (uint8_t)(d[1] << 6 | d[2] << 1 | d[3] >> 4),
+                    (uint8_t)(d[3] << 4 | d[4] >> 1), (uint8_t)(d[4] << 7 | d[5] << 2 | d[6] >> 3),
+                    (uint8_t)(d[6] << 5 | d[7])};
+    int nb = dlen == 8 ? 5 : dlen == 7 ? 4 : dlen == 5 ? 3 : dlen == 4 ? 2 : dlen == 2 ? 1 : 0;
+    out.insert(out.end(), b, b + nb);
+  }
+  return {};
+}
+
+// base64.RawURLEncoding.EncodeToString
+std::string enc_base64(const uint8_t* p, size_t n) {
+  std::string o;
+  o.reserve((n * 8 + 5) / 6);
+  uint32_t acc = 0;
+  int bits = 0;
+  for (size_t i = 0; i < n; i++) {
+    acc = (acc << 8) | p[i];
+    bits += 8;
+    while (bits >= 6) {
+      bits -= 6;
+      o += kB64Url[(acc >> bits) & 63];
+    }
+  }
+  if (bits) o += kB64Url[(acc << (6 - bits)) & 63];
+  return o;
+}
+
+// base64.RawURLEncoding.DecodeString: encoding/base64 decodeQuantum semantics (newlines skipped,
+// no padding, non-strict), CorruptInputError at the offending input byte.
+Err dec_base64(const std::string& s, std::vector<uint8_t>& out) {
+  out.clear();
+  static int8_t map[256];
+  static bool init = false;
+  if (!init) {
+    memset(map, -1, sizeof map);
+    for (int i = 0; i < 64; i++) map[(uint8_t)kB64Url[i]] = (int8_t)i;
+    init = true;
+  }
+  size_t si = 0;
+  while (si < s.size()) {
+    uint8_t d[4] = {0};
+    int dlen = 4;
+    for (int j = 0; j < 4; j++) {
+      if (si == s.size()) {
+        if (j == 0) return {};
+        if (j == 1) return {RC_ERR_BASE64_CORRUPT, (int64_t)si - j};
+        dlen = j;
+        break;
+      }
+      uint8_t in = (uint8_t)s[si++];
+      int8_t v = map[in];
+      if (v >= 0) {
+        d[j] = (uint8_t)v;
+        continue;
+      }
+      if (in == '\n' || in == '\r') {
+        j--;
+        continue;
+      }
+      return {RC_ERR_BASE64_CORRUPT, (int64_t)si - 1};
+    }
+    uint32_t val = (uint32_t)d[0] << 18 | (uint32_t)d[1] << 12 | (uint32_t)d[2] << 6 | d[3];
+    uint8_t b[3] = {(uint8_t)(val >> 16), (uint8_t)(val >> 8), (uint8_t)val};
+    out.insert(out.end(), b, b + (dlen - 1));
+  }
+  return {};
+}
+
+// base32768.SafeEncoding (github.com/Max-Sum/base32768, qntm's base32768): 15 bits per
+// character from a 32768-character repertoire, a final group of <= 7 bits from a
+// 128-character one; bits big-endian, the last group padded with 1s.  The repertoires are
+// ranges of 32 code points given as (first, last) pairs.
+const char32_t kB32768Pairs15[] =
+    U"ҠҿԀԟڀڿݠޟ߀ߟကဟႠႿᄀᅟᆀᆟᇠሿበቿዠዿጠጿᎠᏟᐠᙟᚠᛟកសᠠᡟᣀᣟᦀᦟ᧠᧿ᨠᨿᯀᯟᰀᰟᴀᴟ⇠⇿⋀⋟⍀⏟␀␟─❟➀➿⠀⥿⦠⦿⨠⩟⪀⪿⫠⭟ⰀⰟⲀⳟⴀⴟⵀⵟ⺠⻟㇀㇟㐀䶟䷀龿ꀀꑿ꒠꒿ꔀꗿꙀꙟꚠꛟ꜀ꝟꞀꞟꡀꡟ";
+const char32_t kB32768Pairs7[] = U"ƀƟɀʟ";
+
+struct B32768 {
+  std::vector<char32_t> enc15, enc7;
+  std::vector<int32_t> dec;  // code point (< 0x10000) -> value | (15 or 7) << 16, or -1
+  B32768() {
+    for (size_t i = 0; kB32768Pairs15[i]; i += 2)
+      for (char32_t c = kB32768Pairs15[i]; c <= kB32768Pairs15[i + 1]; c++) enc15.push_back(c);
+    for (size_t i = 0; kB32768Pairs7[i]; i += 2)
+      for (char32_t c = kB32768Pairs7[i]; c <= kB32768Pairs7[i + 1]; c++) enc7.push_back(c);
+    dec.assign(0x10000, -1);
+    for (size_t v = 0; v < enc15.size(); v++) dec[enc15[v]] = (int32_t)v | 15 << 16;
+    for (size_t v = 0; v < enc7.size(); v++) dec[enc7[v]] = (int32_t)v | 7 << 16;
+  }
+};
+const B32768& b32768() {
+  static B32768 t;
+  return t;
+}
+
+std::string enc_base32768(const uint8_t* p, size_t n) {
+  const B32768& t = b32768();
+  std::string o;
+  uint32_t acc = 0;
+  int bits = 0;
+  for (size_t i = 0; i < n; i++) {
+    acc = (acc << 8) | p[i];
+    bits += 8;
+    if (bits >= 15) {
+      bits -= 15;
+      put_rune(o, t.enc15[(acc >> bits) & 0x7FFF]);
+    }
+  }
+  if (bits > 7) {
+    put_rune(o, t.enc15[((acc << (15 - bits)) | ((1u << (15 - bits)) - 1)) & 0x7FFF]);
+  } else if (bits > 0) {
+    put_rune(o, t.enc7[((acc << (7 - bits)) | ((1u << (7 - bits)) - 1)) & 0x7F]);
+  }
+  return o;
+}
+
+// Decoder: a character outside the repertoire, or a 7-bit character before the end, is a
+// CorruptInputError at its character index (cipher_test.go:172-186 pins the index for
+// "㼿c", "!", "㻙ⲿ=㻙ⲿ"); trailing pad bits are dropped.
+Err dec_base32768(const std::string& s, std::vector<uint8_t>& out) {
+  out.clear();
+  const B32768& t = b32768();
+  const uint8_t* p = (const uint8_t*)s.data();
+  size_t i = 0;
+  int64_t idx = 0;
+  uint32_t acc = 0;
+  int bits = 0;
+  bool ended = false;
+  while (i < s.size()) {
+    size_t sz;
+    int32_t r = decode_rune(p + i, s.size() - i, &sz);
+    i += sz;
+    int32_t v = (r >= 0 && r < 0x10000 && !(r == kRuneError && sz == 1)) ? t.dec[r] : -1;
+    if (v < 0 || ended) return {RC_ERR_BASE32768_CORRUPT, idx};
+    int nb = v >> 16;
+    if (nb == 7) ended = true;
+    acc = (acc << nb) | (uint32_t)(v & 0x7FFF);
+    bits += nb;
+    while (bits >= 8) {
+      bits -= 8;
+      out.push_back((uint8_t)(acc >> bits));
+    }
+    acc &= (1u << bits) - 1;
+    idx++;
+  }
+  return {};
+}
+
+std::string encode(int32_t enc, const uint8_t* p, size_t n) {
+  switch (enc) {
+    case RC_ENC_BASE64: return enc_base64(p, n);
+    case RC_ENC_BASE32768: return enc_base32768(p, n);
+    default: return enc_base32(p, n);
+  }
+}
+
+Err decode(int32_t enc, const std::string& s, std::vector<uint8_t>& out) {
+  switch (enc) {
+    case RC_ENC_BASE64: return dec_base64(s, out);
+    case RC_ENC_BASE32768: return dec_base32768(s, out);
+    default: return dec_base32(s, out);
+  }
+}
+
+// ------------------------------------------------------------------ lib/version
+const size_t kVersionLen = 23;  // len("-v2006-01-02-150405.000")
+
+bool is_digit(char c) { return c >= '0' && c <= '9'; }
+
+// version.Match: regexp `-v\d{4}-\d{2}-\d{2}-\d{6}-\d{3}` anywhere in the name.
+bool version_match(const std::string& s) {
+  static const char pat[] = "-vdddd-dd-dd-dddddd-ddd";
+  if (s.size() < kVersionLen) return false;
+  for (size_t st = 0; st + kVersionLen <= s.size(); st++) {
+    size_t k = 0;
+    for (; k < kVersionLen; k++) {
+      char c = s[st + k];
+      if (pat[k] == 'd' ? !is_digit(c) : c != pat[k]) break;
+    }
+    if (k == kVersionLen) return true;
+  }
+  return false;
+}
+
+// path.Ext with splitExt's ".file" rule (version.go:15-25)
+void split_ext(const std::string& name, std::string* base, std::string* ext) {
+  size_t e = std::string::npos;
+  for (size_t i = name.size(); i-- > 0 && name[i] != '/';)
+    if (name[i] == '.') {
+      e = i;
+      break;
+    }
+  if (e == std::string::npos) {
+    *base = name;
+    ext->clear();
+    return;
+  }
+  *ext = name.substr(e);
+  *base = name.substr(0, e);
+  if (base->empty()) std::swap(*base, *ext);
+}
+
+int days_in(int month, int year) {
+  static const int d[] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  if (month == 2 && (year % 4 == 0 && (year % 100 != 0 || year % 400 == 0))) return 29;
+  return d[month - 1];
+}
+
+int num(const std::string& s, size_t at, size_t n) {
+  int v = 0;
+  for (size_t i = 0; i < n; i++) v = v * 10 + (s[at + i] - '0');
+  return v;
+}
+
+// version.Remove (version.go:38-56): the version string is kept verbatim (time.Format of the
+// time time.Parse accepted reproduces it), so Add(name, t) == insert it before the extension.
+bool version_remove(const std::string& name, std::string* stripped, std::string* ver) {
+  std::string base, ext;
+  split_ext(name, &base, &ext);
+  if (base.size() < kVersionLen) return false;
+  size_t st = base.size() - kVersionLen;
+  if (base[base.size() - 4] != '-') return false;
+  // time.Parse("-v2006-01-02-150405.000", ...)
+  const std::string v = base.substr(st);
+  static const char pat[] = "-vdddd-dd-dd-dddddd-ddd";
+  for (size_t k = 0; k < kVersionLen; k++)
+    if (pat[k] == 'd' ? !is_digit(v[k]) : v[k] != pat[k]) return false;
+  int year = num(v, 2, 4), month = num(v, 7, 2), day = num(v, 10, 2);
+  int hh = num(v, 13, 2), mm = num(v, 15, 2), ss = num(v, 17, 2);
+  if (month < 1 || month > 12 || day < 1 || day > days_in(month, year) || hh > 23 || mm > 59 || ss > 59) return false;
+  *stripped = base.substr(0, st) + ext;
+  *ver = v;
+  return true;
+}
+
+std::string version_add(const std::string& name, const std::string& ver) {
+  std::string base, ext;
+  split_ext(name, &base, &ext);
+  return base + ver + ext;
+}
+
+// ------------------------------------------------------------------ obfuscation
+std::string obfuscate(const rc_cipher* c, const std::string& pt) {
+  if (pt.empty()) return "";
+  if (!valid_utf8(pt)) return "!." + pt;
+  int64_t dir = 0;
+  for_runes(pt, [&](int32_t r) { dir += r; });
+  dir %= 256;
+  std::string o = std::to_string(dir) + ".";
+  for (int i = 0; i < 32; i++) dir += c->name_key[i];
+  for_runes(pt, [&](int32_t r) {
+    if (r == '!') {
+      o += "!!";
+    } else if (r >= '0' && r <= '9') {
+      int64_t thisdir = (dir % 9) + 1;
+      put_rune(o, '0' + (r - '0' + thisdir) % 10);
+    } else if ((r >= 'A' && r <= 'Z') || (r >= 'a' && r <= 'z')) {
+      int64_t thisdir = dir % 25 + 1;
+      int64_t pos = r - 'A';
+      if (pos >= 26) pos -= 6;
+      pos = (pos + thisdir) % 52;
+      if (pos >= 26) pos += 6;
+      put_rune(o, 'A' + pos);
+    } else if (r >= 0xA0 && r <= 0xFF) {
+      int64_t thisdir = (dir % 95) + 1;
+      put_rune(o, 0xA0 + (r - 0xA0 + thisdir) % 96);
+    } else if (r >= 0x100) {
+      int64_t thisdir = (dir % 127) + 1;
+      int64_t base = r - r % 256;
+      int64_t nr = base + (r - base + thisdir) % 256;
+      if (!valid_rune(nr)) {
+        o += '!';
+        put_rune(o, r);
+      } else {
+        put_rune(o, nr);
+      }
+    } else {
+      put_rune(o, r);
+    }
+  });
+  return o;
+}
+
+// strconv.Atoi (64-bit int)
+bool atoi64(const std::string& s, int64_t* v) {
+  size_t i = 0;
+  bool neg = false;
+  if (i < s.size() && (s[i] == '+' || s[i] == '-')) neg = s[i++] == '-';
+  if (i == s.size()) return false;
+  uint64_t x = 0;
+  for (; i < s.size(); i++) {
+    if (!is_digit(s[i])) return false;
+    uint64_t d = (uint64_t)(s[i] - '0');
+    if (x > (UINT64_MAX - d) / 10) return false;
+    x = x * 10 + d;
+    if (x > (uint64_t)INT64_MAX + (neg ? 1 : 0)) return false;
+  }
+  *v = neg ? (int64_t)(0 - x) : (int64_t)x;
+  return true;
+}
+
+Err deobfuscate(const rc_cipher* c, const std::string& ct, std::string* out) {
+  out->clear();
+  if (ct.empty()) return {};
+  size_t dot = ct.find('.');
+  if (dot == std::string::npos) return {RC_ERR_NOT_AN_ENCRYPTED_FILE, 0};
+  std::string numstr = ct.substr(0, dot), after = ct.substr(dot + 1);
+  if (numstr == "!") {
+    *out = after;
+    return {};
+  }
+  int64_t dir;
+  if (!atoi64(numstr, &dir)) return {RC_ERR_NOT_AN_ENCRYPTED_FILE, 0};
+  uint64_t udir = (uint64_t)dir;  // Go int arithmetic wraps
+  for (int i = 0; i < 32; i++) udir += c->name_key[i];
+  dir = (int64_t)udir;
+  std::string& o = *out;
+  bool in_quote = false;
+  for_runes(after, [&](int32_t r) {
+    if (in_quote) {
+      put_rune(o, r);
+      in_quote = false;
+    } else if (r == '!') {
+      in_quote = true;
+    } else if (r >= '0' && r <= '9') {
+      int64_t thisdir = (dir % 9) + 1;
+      int64_t nr = '0' + (int64_t)r - '0' - thisdir;
+      if (nr < '0') nr += 10;
+      put_rune(o, nr);
+    } else if ((r >= 'A' && r <= 'Z') || (r >= 'a' && r <= 'z')) {
+      int64_t thisdir = dir % 25 + 1;
+      int64_t pos = r - 'A';
+      if (pos >= 26) pos -= 6;
+      pos -= thisdir;
+      if (pos < 0) pos += 52;
+      if (pos >= 26) pos += 6;
+      put_rune(o, 'A' + pos);
+    } else if (r >= 0xA0 && r <= 0xFF) {
+      int64_t thisdir = (dir % 95) + 1;
+      int64_t nr = 0xA0 + (int64_t)r - 0xA0 - thisdir;
+      if (nr < 0xA0) nr += 96;
+      put_rune(o, nr);
+    } else if (r >= 0x100) {
+      int64_t thisdir = (dir % 127) + 1;
+      int64_t base = r - r % 256;
+      int64_t nr = (int32_t)(base + ((int64_t)r - base - thisdir));
+      if (nr < base) nr += 256;
+      put_rune(o, nr);
+    } else {
+      put_rune(o, r);
+    }
+  });
+  return {};
+}
+
+// ------------------------------------------------------------------ GPU EME engine
+struct NameEngine {
+  std::mutex mu;
+  bool init = false, failed = false;
+  int device = 0;
+  hipStream_t s = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  uint8_t* d_buf = nullptr;
+  size_t d_cap = 0;
+  uint8_t* h_buf = nullptr;  // pinned
+  size_t h_cap = 0;
+};
+
+NameEngine g_names;
+
+bool ne_init(NameEngine& e) {
+  if (e.init) return true;
+  if (e.failed) return false;
+  if (const char* s = getenv("RCLONE_AMD_DEVICE")) e.device = atoi(s);
+  if (hipSetDevice(e.device) != hipSuccess || hipStreamCreateWithFlags(&e.s, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&e.ev0) != hipSuccess || hipEventCreate(&e.ev1) != hipSuccess) {
+    xs::set_error("name engine: no HIP device %d", e.device);
+    e.failed = true;
+    return false;
+  }
+  e.init = true;
+  return true;
+}
+
+bool ne_reserve(NameEngine& e, size_t bytes) {
+  if (bytes <= e.d_cap && bytes <= e.h_cap) return true;
+  size_t cap = e.d_cap ? e.d_cap : (1u << 20);
+  while (cap < bytes) cap *= 2;
+  if (e.d_buf) (void)hipFree(e.d_buf);
+  if (e.h_buf) (void)hipHostFree(e.h_buf);
+  e.d_buf = e.h_buf = nullptr;
+  e.d_cap = e.h_cap = 0;
+  if (hipMalloc(&e.d_buf, cap) != hipSuccess || hipHostMalloc(&e.h_buf, cap, hipHostMallocPortable) != hipSuccess) {
+    xs::set_error("name engine: cannot allocate %zu bytes", cap);
+    return false;
+  }
+  e.d_cap = e.h_cap = cap;
+  return true;
+}
+
+// A batch of segments for the block cipher: padded/decoded bytes packed at 16-aligned
+// offsets, then one H2D, one EME launch (in place), one D2H.
+struct SegBatch {
+  std::vector<uint8_t> data;
+  std::vector<xs_name_desc> desc;
+  uint64_t add(const uint8_t* p, size_t n) {  // n multiple of 16, 16..2048
+    xs_name_desc d{data.size(), (uint32_t)(n / kNameBlock), 0};
+    data.insert(data.end(), p, p + n);
+    desc.push_back(d);
+    return desc.size() - 1;
+  }
+  const uint8_t* get(uint64_t i) const { return data.data() + desc[i].off; }
+};
+
+int32_t run_eme(const rc_cipher* c, bool encrypt, SegBatch& b, double* ms) {
+  *ms = 0;
+  if (b.desc.empty()) return RC_NIL;
+  std::lock_guard<std::mutex> g(g_names.mu);
+  NameEngine& e = g_names;
+  if (!ne_init(e)) return RC_ERR_GPU;
+  size_t data_bytes = b.data.size();
+  size_t desc_off = (data_bytes + 255) & ~(size_t)255;
+  size_t total = desc_off + b.desc.size() * sizeof(xs_name_desc);
+  if (hipSetDevice(e.device) != hipSuccess || !ne_reserve(e, total)) return RC_ERR_GPU;
+  memcpy(e.h_buf, b.data.data(), data_bytes);
+  memcpy(e.h_buf + desc_off, b.desc.data(), b.desc.size() * sizeof(xs_name_desc));
+  hipError_t err = hipMemcpyAsync(e.d_buf, e.h_buf, total, hipMemcpyHostToDevice, e.s);
+  if (err == hipSuccess) err = hipEventRecord(e.ev0, e.s);
+  if (err == hipSuccess)
+    err = xs::launch_eme(encrypt, c->eme, (const xs_name_desc*)(e.d_buf + desc_off), b.desc.size(), e.d_buf, e.d_buf,
+                         data_bytes, e.s);
+  if (err == hipSuccess) err = hipEventRecord(e.ev1, e.s);
+  if (err == hipSuccess) err = hipMemcpyAsync(e.h_buf, e.d_buf, data_bytes, hipMemcpyDeviceToHost, e.s);
+  if (err == hipSuccess) err = hipStreamSynchronize(e.s);
+  if (err != hipSuccess) {
+    xs::set_error("name engine: %s", hipGetErrorString(err));
+    return RC_ERR_GPU;
+  }
+  float f = 0;
+  if (hipEventElapsedTime(&f, e.ev0, e.ev1) == hipSuccess) *ms = f;
+  memcpy(b.data.data(), e.h_buf, data_bytes);
+  return RC_NIL;
+}
+
+// ------------------------------------------------------------------ paths
+struct Seg {
+  std::string text;      // plaintext / ciphertext segment (version stripped)
+  std::string ver;       // version string to add back ("" = none)
+  bool has_ver = false;
+  bool process = false;  // segment is transformed (dirNameEncrypt / last segment)
+  bool gpu = false;      // goes through the EME batch
+  uint64_t slot = 0;     // index in the SegBatch
+  Err err;
+  std::string out;
+};
+
+struct Job {
+  std::vector<Seg> segs;
+  std::string out;  // result when no per-segment work remains (off mode, dir name pass-through)
+  bool direct = false;
+  Err err;
+};
+
+std::vector<std::string> split_path(const std::string& s) {
+  std::vector<std::string> v;
+  size_t st = 0;
+  for (;;) {
+    size_t p = s.find('/', st);
+    if (p == std::string::npos) {
+      v.push_back(s.substr(st));
+      return v;
+    }
+    v.push_back(s.substr(st, p - st));
+    st = p + 1;
+  }
+}
+
+// encryptSegment's host half before the kernel: pkcs7.Pad and pack.
+void seg_encrypt_prepare(Seg& g, SegBatch& b) {
+  if (g.text.empty()) return;  // "" -> ""
+  size_t n = g.text.size();
+  size_t padded = n + (kNameBlock - n % kNameBlock);
+  if (padded > kMaxCipherName) {  // eme.Transform panics on > 128 blocks
+    g.err = {RC_ERR_NAME_TOO_LONG, 0};
+    return;
+  }
+  std::vector<uint8_t> buf(padded, (uint8_t)(padded - n));
+  memcpy(buf.data(), g.text.data(), n);
+  g.slot = b.add(buf.data(), padded);
+  g.gpu = true;
+}
+
+// decryptSegment's host half before the kernel (cipher.go:293-307): decode, length checks.
+void seg_decrypt_prepare(const rc_cipher* c, Seg& g, SegBatch& b) {
+  if (g.text.empty()) return;
+  std::vector<uint8_t> raw;
+  g.err = decode(c->name_enc, g.text, raw);
+  if (g.err.code != RC_NIL) return;
+  if (raw.size() % kNameBlock) {
+    g.err = {RC_ERR_NOT_A_MULTIPLE_OF_BLOCKSIZE, 0};
+    return;
+  }
+  if (raw.empty()) {
+    g.err = {RC_ERR_TOO_SHORT_AFTER_DECODE, 0};
+    return;
+  }
+  if (raw.size() > kMaxCipherName) {
+    g.err = {RC_ERR_TOO_LONG_AFTER_DECODE, 0};
+    return;
+  }
+  g.slot = b.add(raw.data(), raw.size());
+  g.gpu = true;
+}
+
+void seg_encrypt_finish(const rc_cipher* c, Seg& g, const SegBatch& b) {
+  if (!g.gpu) return;
+  const xs_name_desc& d = b.desc[g.slot];
+  g.out = encode(c->name_enc, b.get(g.slot), (size_t)d.nblk * kNameBlock);
+}
+
+// pkcs7.Unpad(16, ...) after the kernel
+void seg_decrypt_finish(Seg& g, const SegBatch& b) {
+  if (!g.gpu) return;
+  const uint8_t* p = b.get(g.slot);
+  size_t len = (size_t)b.desc[g.slot].nblk * kNameBlock;
+  int pad = p[len - 1];
+  if (pad > kNameBlock) {
+    g.err = {RC_ERR_PKCS7_TOO_LONG, 0};
+    return;
+  }
+  if (pad == 0) {
+    g.err = {RC_ERR_PKCS7_TOO_SHORT, 0};
+    return;
+  }
+  for (int i = 0; i < pad; i++)
+    if (p[len - 1 - i] != pad) {
+      g.err = {RC_ERR_PKCS7_NOT_ALL_THE_SAME, 0};
+      return;
+    }
+  g.out.assign((const char*)p, len - pad);
+}
+
+}  // namespace
+
+struct rc_names {
+  std::vector<std::string> s;
+  std::vector<Err> err;
+  double kernel_ms = 0;
+};
+
+extern "C" {
+
+int32_t rc_new_name_encryption_mode(const char* s, int32_t* mode) {
+  std::string v = s ? s : "";
+  for (auto& ch : v) ch = (char)tolower((unsigned char)ch);
+  if (v == "off") *mode = RC_NAME_OFF;
+  else if (v == "standard") *mode = RC_NAME_STANDARD;
+  else if (v == "obfuscate") *mode = RC_NAME_OBFUSCATE;
+  else return RC_ERR_UNKNOWN_MODE;
+  return RC_NIL;
+}
+
+int32_t rc_new_name_encoding(const char* s, int32_t* enc) {
+  std::string v = s ? s : "";
+  for (auto& ch : v) ch = (char)tolower((unsigned char)ch);
+  if (v == "base32") *enc = RC_ENC_BASE32;
+  else if (v == "base64") *enc = RC_ENC_BASE64;
+  else if (v == "base32768") *enc = RC_ENC_BASE32768;
+  else return RC_ERR_UNKNOWN_ENCODING;
+  return RC_NIL;
+}
+
+void rc_cipher_set_name_encryption(rc_cipher* c, int32_t mode, int32_t dir_name_encrypt, int32_t enc) {
+  c->mode = mode;
+  c->dir_name_encrypt = dir_name_encrypt != 0;
+  c->name_enc = enc;
+}
+
+// setEncryptedSuffix (cipher.go:207-217)
+void rc_cipher_set_encrypted_suffix(rc_cipher* c, const char* suffix) {
+  std::string s = suffix ? suffix : "";
+  std::string low = s;
+  for (auto& ch : low) ch = (char)tolower((unsigned char)ch);
+  if (low == "none") {
+    c->encrypted_suffix.clear();
+    return;
+  }
+  if (s.empty() || s[0] != '.') s = "." + s;  // the reference logs ErrorSuffixMissingDot
+  c->encrypted_suffix = s;
+}
+
+int64_t rc_name_encode(int32_t enc, const uint8_t* src, uint64_t n, char* out, uint64_t cap) {
+  std::string s = encode(enc, src, n);
+  if (out) memcpy(out, s.data(), s.size() < cap ? s.size() : cap);
+  return (int64_t)s.size();
+}
+
+int32_t rc_name_decode(int32_t enc, const char* s, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len,
+                       int64_t* err_arg) {
+  std::vector<uint8_t> v;
+  Err e = decode(enc, std::string(s ? s : "", n), v);
+  if (out) memcpy(out, v.data(), v.size() < cap ? v.size() : cap);
+  if (out_len) *out_len = v.size();
+  if (err_arg) *err_arg = e.arg;
+  return e.code;
+}
+
+int xs_eme_batch_dev(int encrypt, const uint8_t name_key[32], const uint8_t tweak[16], const xs_name_desc* d_desc,
+                     uint64_t n, const void* d_src, void* d_dst, uint64_t buf_len, void* stream) {
+  if (!name_key || !tweak || (n && (!d_desc || !d_src || !d_dst))) {
+    xs::set_error("xs_eme_batch_dev: null argument");
+    return XS_ERR_INVALID;
+  }
+  xs::aes::EmeKey k;
+  xs::aes::expand_key(name_key, tweak, &k);
+  hipError_t e = xs::launch_eme(encrypt != 0, k, d_desc, n, (const uint8_t*)d_src, (uint8_t*)d_dst, buf_len,
+                                (hipStream_t)stream);
+  if (e != hipSuccess) {
+    xs::set_error("eme launch: %s", hipGetErrorString(e));
+    return XS_ERR_HIP;
+  }
+  return XS_OK;
+}
+
+int32_t rc_names_run(rc_cipher* c, int32_t op, uint64_t n, const char* const* in, const uint64_t* in_len,
+                     rc_names** out) {
+  if (!c || !out || (n && (!in || !in_len)) || op < 0 || op > RC_OP_DEOBFUSCATE_SEGMENT) return RC_ERR_INVALID;
+  *out = nullptr;
+  const bool enc_dir = op == RC_OP_ENCRYPT_FILE_NAME || op == RC_OP_ENCRYPT_DIR_NAME || op == RC_OP_ENCRYPT_SEGMENT ||
+                       op == RC_OP_OBFUSCATE_SEGMENT;
+  std::vector<Job> jobs(n);
+  SegBatch batch;
+  for (uint64_t i = 0; i < n; i++) {
+    std::string s(in[i] ? in[i] : "", in_len[i]);
+    Job& j = jobs[i];
+    switch (op) {
+      case RC_OP_ENCRYPT_SEGMENT:
+      case RC_OP_DECRYPT_SEGMENT:
+      case RC_OP_OBFUSCATE_SEGMENT:
+      case RC_OP_DEOBFUSCATE_SEGMENT: {
+        Seg g;
+        g.text = s;
+        g.process = true;
+        j.segs.push_back(std::move(g));
+        break;
+      }
+      case RC_OP_ENCRYPT_FILE_NAME:
+        if (c->mode == RC_NAME_OFF) {  // EncryptFileName :542-547
+          j.direct = true;
+          j.out = s + c->encrypted_suffix;
+        }
+        break;
+      case RC_OP_ENCRYPT_DIR_NAME:
+      case RC_OP_DECRYPT_DIR_NAME:
+        if (c->mode == RC_NAME_OFF || !c->dir_name_encrypt) {  // :550-555, :613-618
+          j.direct = true;
+          j.out = s;
+        }
+        break;
+      case RC_OP_DECRYPT_FILE_NAME:
+        if (c->mode == RC_NAME_OFF) {  // DecryptFileName :600-611
+          j.direct = true;
+          size_t sl = c->encrypted_suffix.size();
+          bool has = s.size() >= sl && s.compare(s.size() - sl, sl, c->encrypted_suffix) == 0;
+          if (s.size() == sl || !has) {
+            j.err = {RC_ERR_NOT_AN_ENCRYPTED_FILE, 0};
+          } else {
+            std::string dec = s.substr(0, s.size() - sl);
+            std::string stripped, ver;
+            if (version_match(dec)) {
+              if (!version_remove(dec, &stripped, &ver)) stripped = dec;
+              if (stripped.empty()) j.err = {RC_ERR_NOT_AN_ENCRYPTED_FILE, 0};
+            }
+            if (j.err.code == RC_NIL) j.out = dec;
+          }
+        }
+        break;
+    }
+    if (j.direct || !j.segs.empty()) continue;
+    // encryptFileName / decryptFileName (:482-539, :558-598)
+    std::vector<std::string> parts = split_path(s);
+    j.segs.resize(parts.size());
+    for (size_t k = 0; k < parts.size(); k++) {
+      Seg& g = j.segs[k];
+      g.text = parts[k];
+      bool last = k + 1 == parts.size();
+      g.process = c->dir_name_encrypt || last;
+      if (!g.process) continue;
+      if (last && version_match(g.text)) {
+        std::string stripped, ver;
+        if (version_remove(g.text, &stripped, &ver) && stripped != g.text) {
+          g.text = stripped;
+          g.ver = ver;
+          g.has_ver = true;
+        }
+      }
+    }
+  }
+  // host half before the kernel
+  const bool standard = op == RC_OP_ENCRYPT_SEGMENT || op == RC_OP_DECRYPT_SEGMENT ||
+                        ((op == RC_OP_ENCRYPT_FILE_NAME || op == RC_OP_DECRYPT_FILE_NAME || op == RC_OP_ENCRYPT_DIR_NAME ||
+                          op == RC_OP_DECRYPT_DIR_NAME) &&
+                         c->mode == RC_NAME_STANDARD);
+  for (auto& j : jobs) {
+    if (j.direct) continue;
+    for (auto& g : j.segs) {
+      if (!g.process) continue;
+      if (standard) {
+        if (enc_dir)
+          seg_encrypt_prepare(g, batch);
+        else
+          seg_decrypt_prepare(c, g, batch);
+      } else if (enc_dir) {
+        g.out = obfuscate(c, g.text);
+      } else {
+        g.err = deobfuscate(c, g.text, &g.out);
+      }
+    }
+  }
+  rc_names* r = new rc_names();
+  int32_t rc = run_eme(c, enc_dir, batch, &r->kernel_ms);
+  if (rc != RC_NIL) {
+    delete r;
+    return rc;
+  }
+  r->s.resize(n);
+  r->err.resize(n);
+  for (uint64_t i = 0; i < n; i++) {
+    Job& j = jobs[i];
+    if (j.direct) {
+      r->err[i] = j.err;
+      if (j.err.code == RC_NIL) r->s[i] = std::move(j.out);
+      continue;
+    }
+    std::string res;
+    Err first;
+    for (size_t k = 0; k < j.segs.size(); k++) {
+      Seg& g = j.segs[k];
+      if (g.process && g.gpu) {
+        if (enc_dir)
+          seg_encrypt_finish(c, g, batch);
+        else
+          seg_decrypt_finish(g, batch);
+      }
+      if (g.process && g.err.code != RC_NIL) {  // the first failing segment's error wins
+        first = g.err;
+        break;
+      }
+      std::string piece = g.process ? g.out : g.text;
+      if (g.has_ver) piece = version_add(piece, g.ver);
+      if (k) res += '/';
+      res += piece;
+    }
+    r->err[i] = first;
+    if (first.code == RC_NIL) r->s[i] = std::move(res);
+  }
+  *out = r;
+  return RC_NIL;
+}
+
+void rc_names_get(const rc_names* r, uint64_t i, const char** s, uint64_t* len, int32_t* err, int64_t* err_arg) {
+  if (s) *s = r->s[i].data();
+  if (len) *len = r->s[i].size();
+  if (err) *err = r->err[i].code;
+  if (err_arg) *err_arg = r->err[i].arg;
+}
+
+double rc_names_kernel_ms(const rc_names* r) { return r->kernel_ms; }
+
+void rc_names_free(rc_names* r) { delete r; }
+
+}  // extern "C"

@@ -1,0 +1,240 @@
+"""File-name cipher on the CPU side: the oracle pinned to the reference's vectors, and the host
+logic of the name path (encodings, obfuscation, mode "off", versions) run the way the
+reference's own tests run it (backend/crypt/cipher_test.go:21-683).  Nothing here launches a
+kernel: only standard-mode segments go to the GPU (tests/test_names_gpu.py).
+"""
+import base64
+import json
+import os
+
+import pytest
+
+from oracle import pyoracle as orc
+from rclone_amd import crypt, names
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "name_vectors.json")
+
+
+@pytest.fixture(scope="module")
+def nv():
+    with open(GOLDEN, encoding="utf-8") as f:
+        return json.load(f)
+
+
+# ------------------------------------------------------------------ oracle pinning
+def test_oracle_aes_known_answers(nv):
+    v = nv["fips197_c3"]
+    assert orc.aes256_encrypt(bytes.fromhex(v["key"]), bytes.fromhex(v["pt"])).hex() == v["ct"]
+    for row in nv["aes256"]:
+        key, pt, ct = (bytes.fromhex(row[k]) for k in ("key", "pt", "ct"))
+        for i in range(0, len(pt), 16):
+            assert orc.aes256_encrypt(key, pt[i:i + 16]) == ct[i:i + 16]
+            assert orc.aes256_decrypt(key, ct[i:i + 16]) == pt[i:i + 16]
+
+
+def _b32(b):
+    return base64.b32hexencode(b).decode().rstrip("=").lower()
+
+
+def _b64(b):
+    return base64.urlsafe_b64encode(b).decode().rstrip("=")
+
+
+@pytest.mark.parametrize("enc", ["base32", "base64", "base32768"])
+def test_oracle_eme_against_reference_segments(nv, enc):
+    # TestEncryptSegment* (cipher_test.go:207-271): password "" -> zero nameKey and nameTweak
+    encode = {"base32": _b32, "base64": _b64,
+              "base32768": names.new_name_encoding("base32768").encode_to_string}[enc]
+    for plain, want in nv["segment_" + enc]:
+        if plain == "":
+            continue
+        ct = orc.eme_transform(bytes(32), bytes(16), orc.pkcs7_pad(plain.encode()), True)
+        assert encode(ct) == want, plain
+        assert orc.pkcs7_unpad(orc.eme_transform(bytes(32), bytes(16), ct, False)) == plain.encode()
+
+
+def test_oracle_eme_round_trip_all_lengths():
+    key, tweak = bytes(range(32)), bytes(range(100, 116))
+    for m in (1, 2, 3, 16, 17, 127, 128):
+        data = bytes((i * 7 + m) & 255 for i in range(16 * m))
+        ct = orc.eme_transform(key, tweak, data, True)
+        assert ct != data and orc.eme_transform(key, tweak, ct, False) == data
+    with pytest.raises(ValueError):
+        orc.eme_transform(key, tweak, bytes(16 * 129), True)
+
+
+# ------------------------------------------------------------------ modes and encodings
+def test_new_name_encryption_mode():
+    # TestNewNameEncryptionMode (:21-40), TestNewNameEncryptionModeString (:42-48)
+    for s, want in [("off", 0), ("standard", 1), ("obfuscate", 2), ("OFF", 0), ("Standard", 1)]:
+        assert names.new_name_encryption_mode(s) == want
+    with pytest.raises(ValueError, match='unknown file name encryption mode "potato"'):
+        names.new_name_encryption_mode("potato")
+    assert [names.name_encryption_mode_string(m) for m in (0, 1, 2, 3)] == ["off", "standard", "obfuscate",
+                                                                            "Unknown mode #3"]
+
+
+@pytest.mark.parametrize("enc", ["base32", "base64", "base32768"])
+def test_encode_file_name(nv, enc):
+    # TestEncodeFileNameBase32/64/32768 (:72-136) via testEncodeFileName (:50-70)
+    e = names.new_name_encoding(enc)
+    for plain, want in nv["encode_" + enc]:
+        assert e.encode_to_string(plain.encode()) == want
+        assert e.decode_string(want) == plain.encode()
+        if enc == "base32":
+            assert e.decode_string(want.upper()) == plain.encode()
+
+
+@pytest.mark.parametrize("enc,cases", [
+    ("base32", [("64=", names.ErrorBadBase32Encoding()), ("!", names.Base32CorruptInputError(0)),
+                ("hello=hello", names.Base32CorruptInputError(5))]),
+    ("base64", [("64=", names.Base64CorruptInputError(2)), ("!", names.Base64CorruptInputError(0)),
+                ("Hello=Hello", names.Base64CorruptInputError(5))]),
+    ("base32768", [("㼿c", names.Base32768CorruptInputError(1)), ("!", names.Base32768CorruptInputError(0)),
+                   ("㻙ⲿ=㻙ⲿ", names.Base32768CorruptInputError(2))]),
+])
+def test_decode_file_name_errors(enc, cases):
+    # TestDecodeFileNameBase32/64/32768 (:138-186)
+    e = names.new_name_encoding(enc)
+    for s, want in cases:
+        with pytest.raises(names.NameError_) as ex:
+            e.decode_string(s)
+        assert ex.value == want, s
+
+
+def test_unknown_encoding():
+    with pytest.raises(ValueError, match='unknown file name encoding mode "base99"'):
+        names.new_name_encoding("base99")
+
+
+def test_base64_base32_match_stdlib_random():
+    import random
+    rng = random.Random(5)
+    b32, b64 = names.new_name_encoding("base32"), names.new_name_encoding("base64")
+    for n in range(0, 80):
+        data = bytes(rng.randrange(256) for _ in range(n))
+        assert b32.encode_to_string(data) == _b32(data)
+        assert b64.encode_to_string(data) == _b64(data)
+        assert b32.decode_string(_b32(data)) == data and b64.decode_string(_b64(data)) == data
+
+
+def test_base32768_round_trip_and_length():
+    import random
+    rng = random.Random(6)
+    e = names.new_name_encoding("base32768")
+    for n in range(0, 70):
+        data = bytes(rng.randrange(256) for _ in range(n))
+        s = e.encode_to_string(data)
+        assert len(s) == (8 * n + 14) // 15
+        assert e.decode_string(s) == data
+
+
+# ------------------------------------------------------------------ host-only modes
+def _c(mode, dir_encrypt=True, enc=None):
+    return crypt.new_cipher(mode, "", "", dir_encrypt, enc)
+
+
+def test_non_standard_encrypt_file_name():
+    # TestNonStandardEncryptFileName (:404-431)
+    c = _c(names.NAME_ENCRYPTION_OFF)
+    assert c.encrypt_file_name("1/12/123") == "1/12/123.bin"
+    c.set_encrypted_suffix(".jpg")
+    assert c.encrypt_file_name("1/12/123") == "1/12/123.jpg"
+    c.set_encrypted_suffix("none")
+    assert c.encrypt_file_name("1/12/123") == "1/12/123"
+    c = _c(names.NAME_ENCRYPTION_OBFUSCATED)
+    assert c.encrypt_file_name("1/12/123/!hello") == "49.6/99.23/150.890/53.!!lipps"
+    assert c.encrypt_file_name("1/12/123/!hello-v2001-02-03-040506-123") == \
+        "49.6/99.23/150.890/53-v2001-02-03-040506-123.!!lipps"
+    assert c.encrypt_file_name("1/12/123/hello-v2001-02-03-040506-123.txt") == \
+        "49.6/99.23/150.890/162.uryyB-v2001-02-03-040506-123.GKG"
+    assert c.encrypt_file_name("¡") == "161.ä"
+    assert c.encrypt_file_name("Π") == "160.ς"
+    c = _c(names.NAME_ENCRYPTION_OBFUSCATED, False)
+    assert c.encrypt_file_name("1/12/123/!hello") == "1/12/123/53.!!lipps"
+    assert c.encrypt_file_name("1/12/123/!hello-v2001-02-03-040506-123") == \
+        "1/12/123/53-v2001-02-03-040506-123.!!lipps"
+    assert c.encrypt_file_name("¡") == "161.ä"
+    assert c.encrypt_file_name("Π") == "160.ς"
+
+
+@pytest.mark.parametrize("enc", ["base32", "base64", "base32768"])
+def test_non_standard_decrypt_file_name(enc):
+    # TestNonStandardDecryptFileName (:484-520)
+    E = names.new_name_encoding(enc)
+    OFF, OBF = names.NAME_ENCRYPTION_OFF, names.NAME_ENCRYPTION_OBFUSCATED
+    for mode, dir_enc, inp, want, err, suffix in [
+        (OFF, True, "1/12/123.bin", "1/12/123", None, ""),
+        (OFF, True, "1/12/123.bix", "", names.ErrorNotAnEncryptedFile(), ""),
+        (OFF, True, ".bin", "", names.ErrorNotAnEncryptedFile(), ""),
+        (OFF, True, "1/12/123-v2001-02-03-040506-123.bin", "1/12/123-v2001-02-03-040506-123", None, ""),
+        (OFF, True, "1/12/123-v1970-01-01-010101-123-v2001-02-03-040506-123.bin",
+         "1/12/123-v1970-01-01-010101-123-v2001-02-03-040506-123", None, ""),
+        (OFF, True, "1/12/123-v1970-01-01-010101-123-v2001-02-03-040506-123.txt.bin",
+         "1/12/123-v1970-01-01-010101-123-v2001-02-03-040506-123.txt", None, ""),
+        (OFF, True, "1/12/123.jpg", "1/12/123", None, ".jpg"),
+        (OFF, True, "1/12/123", "1/12/123", None, "none"),
+        (OBF, True, "!.hello", "hello", None, ""),
+        (OBF, True, "hello", "", names.ErrorNotAnEncryptedFile(), ""),
+        (OBF, True, "161.ä", "¡", None, ""),
+        (OBF, True, "160.ς", "Π", None, ""),
+        (OBF, False, "1/12/123/53.!!lipps", "1/12/123/!hello", None, ""),
+        (OBF, False, "1/12/123/53-v2001-02-03-040506-123.!!lipps", "1/12/123/!hello-v2001-02-03-040506-123", None, ""),
+    ]:
+        c = _c(mode, dir_enc, E)
+        if suffix:
+            c.set_encrypted_suffix(suffix)
+        if err is None:
+            assert c.decrypt_file_name(inp) == want, inp
+        else:
+            with pytest.raises(names.NameError_) as ex:
+                c.decrypt_file_name(inp)
+            assert ex.value == err, inp
+
+
+@pytest.mark.parametrize("enc", ["base32", "base64", "base32768"])
+def test_enc_dec_matches_host_modes(enc):
+    # TestEncDecMatches (:522-550), the modes that need no block cipher
+    E = names.new_name_encoding(enc)
+    for mode, s in [(names.NAME_ENCRYPTION_OFF, "1/2/3/4"),
+                    (names.NAME_ENCRYPTION_OBFUSCATED, "1/2/3/4/!helloΠ"),
+                    (names.NAME_ENCRYPTION_OBFUSCATED, "Avatar The Last Airbender")]:
+        c = _c(mode, True, E)
+        assert c.decrypt_file_name(c.encrypt_file_name(s)) == s
+
+
+def test_non_standard_dir_names_off():
+    # TestNonStandardEncryptDirName off part (:576-587), TestNonStandardDecryptDirName (:665-683)
+    for enc in ("base32", "base64", "base32768"):
+        E = names.new_name_encoding(enc)
+        c = _c(names.NAME_ENCRYPTION_STANDARD, False, E)
+        assert c.encrypt_dir_name("1/12") == "1/12"
+        assert c.encrypt_dir_name("1/12/123") == "1/12/123"
+        c = _c(names.NAME_ENCRYPTION_OFF, True, E)
+        assert c.encrypt_dir_name("1/12/123") == "1/12/123"
+    for s in ("1/12/123.bin", "1/12/123", ".bin"):
+        assert _c(names.NAME_ENCRYPTION_OFF).decrypt_dir_name(s) == s
+
+
+def test_obfuscate_round_trip_unicode_and_invalid_utf8():
+    import random
+    rng = random.Random(9)
+    c = _c(names.NAME_ENCRYPTION_OBFUSCATED, True)
+    c.key("potato")
+    alphabet = "abcXYZ0189!. _- éÿĀΠ中퟿\U0001f600"
+    batch = ["".join(rng.choice(alphabet) for _ in range(rng.randrange(1, 30))) for _ in range(300)]
+    enc = c.encrypt_file_names(batch)
+    assert c.decrypt_file_names(enc) == batch
+    # invalid UTF-8 is prefixed with "!." and passes through unchanged
+    bad = b"ab\xffcd".decode("utf-8", "surrogateescape")
+    assert c.obfuscate_segment(bad) == "!." + bad
+    assert c.deobfuscate_segment("!." + bad) == bad
+
+
+def test_version_strip_only_valid_dates():
+    c = _c(names.NAME_ENCRYPTION_OBFUSCATED, True)
+    ok = c.encrypt_file_name("a-v2024-02-29-235959-999.txt")  # leap day: a version
+    assert "-v2024-02-29-235959-999" in ok and not ok.startswith("-v")
+    bad = c.encrypt_file_name("a-v2023-02-29-235959-999.txt")  # no Feb 29 in 2023: not a version
+    assert "-v2023" not in bad
+    assert c.decrypt_file_name(bad) == "a-v2023-02-29-235959-999.txt"
