@@ -51,6 +51,10 @@ def parse():
                     help="configs[3] mode: one logical object of this many blocks (2^24 = 1 TiB) split "
                          "round-robin over the ranks, processed in --blocks rounds with on-device "
                          "generation inside each step (0 = the default resident-set bench)")
+    ap.add_argument("--names", type=int, default=0,
+                    help="file-name mode (SURVEY 8(f) rank 4): encrypt + decrypt this many names per step "
+                         "through rc_names_run (0 = the default crypt-block bench)")
+    ap.add_argument("--name-paths", action="store_true", help="names mode: 3-segment paths instead of one segment")
     return ap.parse_args()
 
 
@@ -185,6 +189,126 @@ def run_objectset(args, world, rank, dev, dist):
         dist.destroy_process_group()
 
 
+def names_cpu_baseline(segs, key, tweak, seconds):
+    """Oracle EME (oracle/eme_oracle.c) over a bounded sample, one core, C loop per name."""
+    from oracle import pyoracle as orc  # checker/baseline only
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < seconds:
+        orc.eme_transform(key, tweak, orc.pkcs7_pad(segs[k % len(segs)]), True)
+        k += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(k / dt), "unit": "names/s", "cores": 1, "kind": "port",
+            "sample": f"{k} single-segment names encrypted by oracle/eme_oracle.c in {dt:.1f} s "
+                      "(one ctypes call per name; EME only, no encoding)"}
+
+
+def run_names(args, world, rank):
+    """configs-independent secondary bench: batched file-name encryption (EME-AES-256 + pkcs7 +
+    base32) and decryption of a synthetic listing, through the C ABI (rc_names_run).  One step =
+    encrypt N names then decrypt them; value = names/s both directions counted, summed over ranks
+    (each rank its own listing, weak scaling).  The EME kernel's own time comes from HIP events
+    inside rc_names_run."""
+    import numpy as np
+    import torch
+    from rclone_amd import _lib, crypt, names
+    L = _lib.lib()
+    n = args.names
+    rng = np.random.default_rng(1000 + rank)
+    lens = rng.integers(8, 65, n)
+    pool = rng.integers(ord("a"), ord("z") + 1, int(lens.sum()), dtype=np.uint8).tobytes()
+    segs, p = [], 0
+    for ln in lens:
+        segs.append(pool[p:p + ln])
+        p += ln
+    if args.name_paths:
+        inp = [b"dir%03d/sub%04d/" % (i % 997, i % 7919) + s for i, s in enumerate(segs)]
+    else:
+        inp = segs
+    c = crypt.new_cipher(names.NAME_ENCRYPTION_STANDARD, "potato", "", True, names.new_name_encoding("base32"))
+
+    def carr(lst):
+        a = (ctypes.c_char_p * n)(*lst)
+        ln = (ctypes.c_uint64 * n)(*[len(x) for x in lst])
+        return a, ln
+
+    def run(op, arr, lens_):
+        out = ctypes.c_void_p()
+        rc = L.rc_names_run(c._h, op, n, arr, lens_, ctypes.byref(out))
+        if rc != 0:
+            raise SystemExit(f"rc_names_run failed: {rc} {_lib.last_error()}")
+        return out
+
+    def collect(h):
+        vals = []
+        ptr, ln, err, arg = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_int32(), ctypes.c_int64()
+        for i in range(n):
+            L.rc_names_get(h, i, ctypes.byref(ptr), ctypes.byref(ln), ctypes.byref(err), ctypes.byref(arg))
+            if err.value:
+                raise SystemExit(f"name {i}: error {err.value}")
+            vals.append(ctypes.string_at(ptr.value, ln.value))
+        return vals
+
+    op_e = names.OP_ENCRYPT_FILE_NAME
+    op_d = names.OP_DECRYPT_FILE_NAME
+    pa, pl = carr(inp)
+    h = run(op_e, pa, pl)
+    enc = collect(h)
+    L.rc_names_free(h)
+    ea, el_ = carr(enc)
+    h = run(op_d, ea, el_)
+    if collect(h) != inp:
+        raise SystemExit("names: round trip failed")
+    L.rc_names_free(h)
+    for _ in range(args.warmup):
+        L.rc_names_free(run(op_e, pa, pl))
+        L.rc_names_free(run(op_d, ea, el_))
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    k_e, k_d, t_e, t_d = [], [], [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        a = time.perf_counter()
+        h = run(op_e, pa, pl)
+        k_e.append(L.rc_names_kernel_ms(h))
+        L.rc_names_free(h)
+        b = time.perf_counter()
+        h = run(op_d, ea, el_)
+        k_d.append(L.rc_names_kernel_ms(h))
+        L.rc_names_free(h)
+        t_e.append(b - a)
+        t_d.append(time.perf_counter() - b)
+    el = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        padded = int(((lens // 16) + 1).sum()) * 16
+        ke, kd = float(np.mean(k_e)), float(np.mean(k_d))
+        res = {
+            "metric": "file names/s, crypt EME-AES-256 name encrypt+decrypt (rc_names_run, host-resident)",
+            "value": round(2 * n * args.steps * world / el), "unit": "names/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (lowercase names, 8-64 bytes)",
+            "config": {"workload": f"{n} {'3-segment paths' if args.name_paths else 'names'} per rank, "
+                                   "EncryptFileName then DecryptFileName, base32, standard mode",
+                       "names_per_rank": n, "paths": bool(args.name_paths)},
+            "encrypt_s": round(float(np.mean(t_e)), 4), "decrypt_s": round(float(np.mean(t_d)), 4),
+            "kernel": {"encrypt_ms": round(ke, 4), "decrypt_ms": round(kd, 4),
+                       "segments_per_launch": n * (3 if args.name_paths else 1),
+                       "segment_bytes_padded": padded,
+                       "kernel_names_per_s": round(n / (ke * 1e-3))},
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu:
+            res["cpu_baseline"] = names_cpu_baseline(segs, c.name_key, c.name_tweak, 5.0)
+        print(json.dumps(res), flush=True)
+
+
 def main():
     args = parse()
     import torch
@@ -201,6 +325,8 @@ def main():
 
     if args.object_blocks:
         return run_objectset(args, world, rank, dev, dist)
+    if args.names:
+        return run_names(args, world, rank)
 
     import numpy as np
 

@@ -19,12 +19,15 @@
 // and which segment's error wins) are the reference's.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rc_internal.h"
@@ -136,9 +139,7 @@ const char kB32Hex[] = "0123456789ABCDEFGHIJKLMNOPQRSTUV";
 const char kB64Url[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
 
 // base32.HexEncoding.EncodeToString, '=' trimmed, lower-cased (cipher.go:136-140).
-std::string enc_base32(const uint8_t* p, size_t n) {
-  std::string o;
-  o.reserve((n * 8 + 4) / 5);
+void enc_base32(const uint8_t* p, size_t n, std::string& o) {
   uint64_t acc = 0;
   int bits = 0;
   for (size_t i = 0; i < n; i++) {
@@ -150,19 +151,20 @@ std::string enc_base32(const uint8_t* p, size_t n) {
     }
   }
   if (bits) o += (char)tolower(kB32Hex[(acc << (5 - bits)) & 31]);
-  return o;
 }
 
 // caseInsensitiveBase32Encoding.DecodeString (cipher.go:143-152) over encoding/base32's
 // decoder: '=' suffix rejected, padding re-added, upper-cased, newlines stripped, then the
 // quantum decoder with Go's CorruptInputError offsets.
-Err dec_base32(const std::string& s0, std::vector<uint8_t>& out) {
+Err dec_base32(const char* s0, size_t n0, std::vector<uint8_t>& out) {
   out.clear();
-  if (!s0.empty() && s0.back() == '=') return {RC_ERR_BAD_BASE32_ENCODING, 0};
-  size_t equals = ((s0.size() + 7) & ~(size_t)7) - s0.size();
-  std::string s;
-  s.reserve(s0.size() + equals);
-  for (char ch : s0) {
+  if (n0 && s0[n0 - 1] == '=') return {RC_ERR_BAD_BASE32_ENCODING, 0};
+  size_t equals = ((n0 + 7) & ~(size_t)7) - n0;
+  thread_local std::string s;
+  s.clear();
+  s.reserve(n0 + equals);
+  for (size_t q = 0; q < n0; q++) {
+    char ch = s0[q];
     if (ch == '\r' || ch == '\n') continue;  // stripNewlines
     s += (ch >= 'a' && ch <= 'z') ? (char)(ch - 32) : ch;
   }
@@ -209,9 +211,7 @@ Err dec_base32(const std::string& s0, std::vector<uint8_t>& out) {
 }
 
 // base64.RawURLEncoding.EncodeToString
-std::string enc_base64(const uint8_t* p, size_t n) {
-  std::string o;
-  o.reserve((n * 8 + 5) / 6);
+void enc_base64(const uint8_t* p, size_t n, std::string& o) {
   uint32_t acc = 0;
   int bits = 0;
   for (size_t i = 0; i < n; i++) {
@@ -223,12 +223,11 @@ std::string enc_base64(const uint8_t* p, size_t n) {
     }
   }
   if (bits) o += kB64Url[(acc << (6 - bits)) & 63];
-  return o;
 }
 
 // base64.RawURLEncoding.DecodeString: encoding/base64 decodeQuantum semantics (newlines skipped,
 // no padding, non-strict), CorruptInputError at the offending input byte.
-Err dec_base64(const std::string& s, std::vector<uint8_t>& out) {
+Err dec_base64(const char* s, size_t sn, std::vector<uint8_t>& out) {
   out.clear();
   static int8_t map[256];
   static bool init = false;
@@ -238,11 +237,11 @@ Err dec_base64(const std::string& s, std::vector<uint8_t>& out) {
     init = true;
   }
   size_t si = 0;
-  while (si < s.size()) {
+  while (si < sn) {
     uint8_t d[4] = {0};
     int dlen = 4;
     for (int j = 0; j < 4; j++) {
-      if (si == s.size()) {
+      if (si == sn) {
         if (j == 0) return {};
         if (j == 1) return {RC_ERR_BASE64_CORRUPT, (int64_t)si - j};
         dlen = j;
@@ -293,9 +292,8 @@ const B32768& b32768() {
   return t;
 }
 
-std::string enc_base32768(const uint8_t* p, size_t n) {
+void enc_base32768(const uint8_t* p, size_t n, std::string& o) {
   const B32768& t = b32768();
-  std::string o;
   uint32_t acc = 0;
   int bits = 0;
   for (size_t i = 0; i < n; i++) {
@@ -311,24 +309,23 @@ std::string enc_base32768(const uint8_t* p, size_t n) {
   } else if (bits > 0) {
     put_rune(o, t.enc7[((acc << (7 - bits)) | ((1u << (7 - bits)) - 1)) & 0x7F]);
   }
-  return o;
 }
 
 // Decoder: a character outside the repertoire, or a 7-bit character before the end, is a
 // CorruptInputError at its character index (cipher_test.go:172-186 pins the index for
 // "㼿c", "!", "㻙ⲿ=㻙ⲿ"); trailing pad bits are dropped.
-Err dec_base32768(const std::string& s, std::vector<uint8_t>& out) {
+Err dec_base32768(const char* s, size_t sn, std::vector<uint8_t>& out) {
   out.clear();
   const B32768& t = b32768();
-  const uint8_t* p = (const uint8_t*)s.data();
+  const uint8_t* p = (const uint8_t*)s;
   size_t i = 0;
   int64_t idx = 0;
   uint32_t acc = 0;
   int bits = 0;
   bool ended = false;
-  while (i < s.size()) {
+  while (i < sn) {
     size_t sz;
-    int32_t r = decode_rune(p + i, s.size() - i, &sz);
+    int32_t r = decode_rune(p + i, sn - i, &sz);
     i += sz;
     int32_t v = (r >= 0 && r < 0x10000 && !(r == kRuneError && sz == 1)) ? t.dec[r] : -1;
     if (v < 0 || ended) return {RC_ERR_BASE32768_CORRUPT, idx};
@@ -346,19 +343,25 @@ Err dec_base32768(const std::string& s, std::vector<uint8_t>& out) {
   return {};
 }
 
-std::string encode(int32_t enc, const uint8_t* p, size_t n) {
+void encode_append(int32_t enc, const uint8_t* p, size_t n, std::string& o) {
   switch (enc) {
-    case RC_ENC_BASE64: return enc_base64(p, n);
-    case RC_ENC_BASE32768: return enc_base32768(p, n);
-    default: return enc_base32(p, n);
+    case RC_ENC_BASE64: return enc_base64(p, n, o);
+    case RC_ENC_BASE32768: return enc_base32768(p, n, o);
+    default: return enc_base32(p, n, o);
   }
 }
 
-Err decode(int32_t enc, const std::string& s, std::vector<uint8_t>& out) {
+std::string encode(int32_t enc, const uint8_t* p, size_t n) {
+  std::string o;
+  encode_append(enc, p, n, o);
+  return o;
+}
+
+Err decode(int32_t enc, const char* p, size_t n, std::vector<uint8_t>& out) {
   switch (enc) {
-    case RC_ENC_BASE64: return dec_base64(s, out);
-    case RC_ENC_BASE32768: return dec_base32768(s, out);
-    default: return dec_base32(s, out);
+    case RC_ENC_BASE64: return dec_base64(p, n, out);
+    case RC_ENC_BASE32768: return dec_base32768(p, n, out);
+    default: return dec_base32(p, n, out);
   }
 }
 
@@ -368,36 +371,25 @@ const size_t kVersionLen = 23;  // len("-v2006-01-02-150405.000")
 bool is_digit(char c) { return c >= '0' && c <= '9'; }
 
 // version.Match: regexp `-v\d{4}-\d{2}-\d{2}-\d{6}-\d{3}` anywhere in the name.
-bool version_match(const std::string& s) {
-  static const char pat[] = "-vdddd-dd-dd-dddddd-ddd";
-  if (s.size() < kVersionLen) return false;
-  for (size_t st = 0; st + kVersionLen <= s.size(); st++) {
-    size_t k = 0;
-    for (; k < kVersionLen; k++) {
-      char c = s[st + k];
-      if (pat[k] == 'd' ? !is_digit(c) : c != pat[k]) break;
-    }
-    if (k == kVersionLen) return true;
-  }
+const char kVersionPat[] = "-vdddd-dd-dd-dddddd-ddd";
+
+bool version_at(const char* p) {
+  for (size_t k = 0; k < kVersionLen; k++)
+    if (kVersionPat[k] == 'd' ? !is_digit(p[k]) : p[k] != kVersionPat[k]) return false;
+  return true;
+}
+
+bool version_match(const char* p, size_t n) {
+  for (size_t st = 0; st + kVersionLen <= n; st++)
+    if (p[st] == '-' && version_at(p + st)) return true;
   return false;
 }
 
-// path.Ext with splitExt's ".file" rule (version.go:15-25)
-void split_ext(const std::string& name, std::string* base, std::string* ext) {
-  size_t e = std::string::npos;
-  for (size_t i = name.size(); i-- > 0 && name[i] != '/';)
-    if (name[i] == '.') {
-      e = i;
-      break;
-    }
-  if (e == std::string::npos) {
-    *base = name;
-    ext->clear();
-    return;
-  }
-  *ext = name.substr(e);
-  *base = name.substr(0, e);
-  if (base->empty()) std::swap(*base, *ext);
+// path.Ext with splitExt's ".file" rule (version.go:15-25): the base length of name.
+size_t base_len(const char* p, size_t n) {
+  for (size_t i = n; i-- > 0 && p[i] != '/';)
+    if (p[i] == '.') return i == 0 ? n : i;  // ".file": base = ".file", ext = ""
+  return n;
 }
 
 int days_in(int month, int year) {
@@ -406,37 +398,34 @@ int days_in(int month, int year) {
   return d[month - 1];
 }
 
-int num(const std::string& s, size_t at, size_t n) {
+int num(const char* s, size_t n) {
   int v = 0;
-  for (size_t i = 0; i < n; i++) v = v * 10 + (s[at + i] - '0');
+  for (size_t i = 0; i < n; i++) v = v * 10 + (s[i] - '0');
   return v;
 }
 
-// version.Remove (version.go:38-56): the version string is kept verbatim (time.Format of the
-// time time.Parse accepted reproduces it), so Add(name, t) == insert it before the extension.
-bool version_remove(const std::string& name, std::string* stripped, std::string* ver) {
-  std::string base, ext;
-  split_ext(name, &base, &ext);
-  if (base.size() < kVersionLen) return false;
-  size_t st = base.size() - kVersionLen;
-  if (base[base.size() - 4] != '-') return false;
-  // time.Parse("-v2006-01-02-150405.000", ...)
-  const std::string v = base.substr(st);
-  static const char pat[] = "-vdddd-dd-dd-dddddd-ddd";
-  for (size_t k = 0; k < kVersionLen; k++)
-    if (pat[k] == 'd' ? !is_digit(v[k]) : v[k] != pat[k]) return false;
-  int year = num(v, 2, 4), month = num(v, 7, 2), day = num(v, 10, 2);
-  int hh = num(v, 13, 2), mm = num(v, 15, 2), ss = num(v, 17, 2);
+// version.Remove (version.go:38-56): if name's base ends in a version time.Parse accepts,
+// returns its position; the stripped name is name[:at] + name[at+23:].  The version string is
+// then kept verbatim (time.Format of the parsed time reproduces it), so version.Add(name, t)
+// == insert it before name's extension.
+bool version_remove(const char* p, size_t n, size_t* at) {
+  size_t bl = base_len(p, n);
+  if (bl < kVersionLen) return false;
+  size_t st = bl - kVersionLen;
+  if (p[bl - 4] != '-') return false;
+  const char* v = p + st;  // time.Parse("-v2006-01-02-150405.000", ...)
+  if (!version_at(v)) return false;
+  int year = num(v + 2, 4), month = num(v + 7, 2), day = num(v + 10, 2);
+  int hh = num(v + 13, 2), mm = num(v + 15, 2), ss = num(v + 17, 2);
   if (month < 1 || month > 12 || day < 1 || day > days_in(month, year) || hh > 23 || mm > 59 || ss > 59) return false;
-  *stripped = base.substr(0, st) + ext;
-  *ver = v;
+  *at = st;
   return true;
 }
 
-std::string version_add(const std::string& name, const std::string& ver) {
-  std::string base, ext;
-  split_ext(name, &base, &ext);
-  return base + ver + ext;
+// version.Add for the piece of `o` starting at `from`: insert ver before the piece's extension.
+void version_add_at(std::string& o, size_t from, const char* ver) {
+  size_t bl = base_len(o.data() + from, o.size() - from);
+  o.insert(from + bl, ver, kVersionLen);
 }
 
 // ------------------------------------------------------------------ obfuscation
@@ -612,22 +601,58 @@ struct SegBatch {
   const uint8_t* get(uint64_t i) const { return data.data() + desc[i].off; }
 };
 
-int32_t run_eme(const rc_cipher* c, bool encrypt, SegBatch& b, double* ms) {
+// Host stages of a large batch run on up to kHostThreads threads, one chunk of names each.
+constexpr size_t kChunkNames = 8192;
+constexpr unsigned kHostThreads = 16;
+
+template <class F>
+void parallel_for(size_t n, F f) {
+  unsigned nt = std::thread::hardware_concurrency();
+  if (const char* e = getenv("RCLONE_AMD_NAME_THREADS")) nt = (unsigned)atoi(e);
+  nt = std::max(1u, std::min({nt, kHostThreads, (unsigned)n}));
+  if (nt <= 1) {
+    for (size_t i = 0; i < n; i++) f(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; t++)
+    th.emplace_back([&] {
+      for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+    });
+  for (auto& t : th) t.join();
+}
+
+// All parts' segments in one pinned buffer -> one H2D, one EME launch (in place), one D2H.
+int32_t run_eme(const rc_cipher* c, bool encrypt, std::vector<SegBatch*>& parts, double* ms) {
   *ms = 0;
-  if (b.desc.empty()) return RC_NIL;
+  size_t nparts = parts.size();
+  std::vector<size_t> base(nparts + 1, 0), dbase(nparts + 1, 0);
+  for (size_t i = 0; i < nparts; i++) {
+    base[i + 1] = base[i] + parts[i]->data.size();
+    dbase[i + 1] = dbase[i] + parts[i]->desc.size();
+  }
+  const size_t data_bytes = base[nparts], ndesc = dbase[nparts];
+  if (ndesc == 0) return RC_NIL;
   std::lock_guard<std::mutex> g(g_names.mu);
   NameEngine& e = g_names;
   if (!ne_init(e)) return RC_ERR_GPU;
-  size_t data_bytes = b.data.size();
   size_t desc_off = (data_bytes + 255) & ~(size_t)255;
-  size_t total = desc_off + b.desc.size() * sizeof(xs_name_desc);
+  size_t total = desc_off + ndesc * sizeof(xs_name_desc);
   if (hipSetDevice(e.device) != hipSuccess || !ne_reserve(e, total)) return RC_ERR_GPU;
-  memcpy(e.h_buf, b.data.data(), data_bytes);
-  memcpy(e.h_buf + desc_off, b.desc.data(), b.desc.size() * sizeof(xs_name_desc));
+  xs_name_desc* hd = (xs_name_desc*)(e.h_buf + desc_off);
+  parallel_for(nparts, [&](size_t i) {
+    const SegBatch& b = *parts[i];
+    memcpy(e.h_buf + base[i], b.data.data(), b.data.size());
+    for (size_t k = 0; k < b.desc.size(); k++) {
+      hd[dbase[i] + k] = b.desc[k];
+      hd[dbase[i] + k].off += base[i];
+    }
+  });
   hipError_t err = hipMemcpyAsync(e.d_buf, e.h_buf, total, hipMemcpyHostToDevice, e.s);
   if (err == hipSuccess) err = hipEventRecord(e.ev0, e.s);
   if (err == hipSuccess)
-    err = xs::launch_eme(encrypt, c->eme, (const xs_name_desc*)(e.d_buf + desc_off), b.desc.size(), e.d_buf, e.d_buf,
+    err = xs::launch_eme(encrypt, c->eme, (const xs_name_desc*)(e.d_buf + desc_off), ndesc, e.d_buf, e.d_buf,
                          data_bytes, e.s);
   if (err == hipSuccess) err = hipEventRecord(e.ev1, e.s);
   if (err == hipSuccess) err = hipMemcpyAsync(e.h_buf, e.d_buf, data_bytes, hipMemcpyDeviceToHost, e.s);
@@ -638,63 +663,62 @@ int32_t run_eme(const rc_cipher* c, bool encrypt, SegBatch& b, double* ms) {
   }
   float f = 0;
   if (hipEventElapsedTime(&f, e.ev0, e.ev1) == hipSuccess) *ms = f;
-  memcpy(b.data.data(), e.h_buf, data_bytes);
+  parallel_for(nparts, [&](size_t i) { memcpy(parts[i]->data.data(), e.h_buf + base[i], parts[i]->data.size()); });
   return RC_NIL;
 }
 
-// ------------------------------------------------------------------ paths
+// ------------------------------------------------------------------ paths (flat, per chunk)
+// A chunk holds up to kChunkNames consecutive inputs of one rc_names_run call: their segments
+// in one vector, owned texts / host-mode outputs / results in a few strings, so a name costs
+// no heap allocations of its own.
 struct Seg {
-  std::string text;      // plaintext / ciphertext segment (version stripped)
-  std::string ver;       // version string to add back ("" = none)
-  bool has_ver = false;
-  bool process = false;  // segment is transformed (dirNameEncrypt / last segment)
-  bool gpu = false;      // goes through the EME batch
-  uint64_t slot = 0;     // index in the SegBatch
+  uint32_t off = 0, len = 0;          // text: [off, off+len) of the input, or of Chunk::own if owned
+  uint32_t ver = 0;                   // version string (23 bytes) at input offset ver when has_ver
+  uint32_t slot = 0;                  // descriptor index in the chunk's SegBatch when gpu
+  uint32_t out_off = 0, out_len = 0;  // obfuscate / deobfuscate output in Chunk::segout
+  bool owned = false, process = false, gpu = false, has_ver = false;
   Err err;
-  std::string out;
 };
 
-struct Job {
+struct Chunk {
   std::vector<Seg> segs;
-  std::string out;  // result when no per-segment work remains (off mode, dir name pass-through)
-  bool direct = false;
-  Err err;
+  std::vector<uint32_t> seg0;  // input k owns segs[seg0[k] .. seg0[k+1])
+  std::vector<uint8_t> direct; // input k was resolved without segments (result already in res)
+  std::string own, segout;
+  SegBatch batch;
+  std::string res;             // every result of the chunk, back to back
+  std::vector<uint64_t> roff;
+  std::vector<uint32_t> rlen;
+  std::vector<Err> err;
 };
 
-std::vector<std::string> split_path(const std::string& s) {
-  std::vector<std::string> v;
-  size_t st = 0;
-  for (;;) {
-    size_t p = s.find('/', st);
-    if (p == std::string::npos) {
-      v.push_back(s.substr(st));
-      return v;
-    }
-    v.push_back(s.substr(st, p - st));
-    st = p + 1;
-  }
-}
+struct Ctx {
+  const rc_cipher* c;
+  int32_t op;
+  bool enc_dir, standard;
+};
 
-// encryptSegment's host half before the kernel: pkcs7.Pad and pack.
-void seg_encrypt_prepare(Seg& g, SegBatch& b) {
-  if (g.text.empty()) return;  // "" -> ""
-  size_t n = g.text.size();
+// pkcs7.Pad(16) straight into the batch (encryptSegment's host half before the kernel).
+void seg_encrypt_prepare(Seg& g, const char* text, SegBatch& b) {
+  size_t n = g.len;
   size_t padded = n + (kNameBlock - n % kNameBlock);
   if (padded > kMaxCipherName) {  // eme.Transform panics on > 128 blocks
     g.err = {RC_ERR_NAME_TOO_LONG, 0};
     return;
   }
-  std::vector<uint8_t> buf(padded, (uint8_t)(padded - n));
-  memcpy(buf.data(), g.text.data(), n);
-  g.slot = b.add(buf.data(), padded);
+  size_t off = b.data.size();
+  b.data.resize(off + padded);
+  memcpy(b.data.data() + off, text, n);
+  memset(b.data.data() + off + n, (int)(padded - n), padded - n);
+  b.desc.push_back(xs_name_desc{off, (uint32_t)(padded / kNameBlock), 0});
+  g.slot = (uint32_t)(b.desc.size() - 1);
   g.gpu = true;
 }
 
 // decryptSegment's host half before the kernel (cipher.go:293-307): decode, length checks.
-void seg_decrypt_prepare(const rc_cipher* c, Seg& g, SegBatch& b) {
-  if (g.text.empty()) return;
-  std::vector<uint8_t> raw;
-  g.err = decode(c->name_enc, g.text, raw);
+void seg_decrypt_prepare(const rc_cipher* c, Seg& g, const char* text, SegBatch& b) {
+  thread_local std::vector<uint8_t> raw;
+  g.err = decode(c->name_enc, text, g.len, raw);
   if (g.err.code != RC_NIL) return;
   if (raw.size() % kNameBlock) {
     g.err = {RC_ERR_NOT_A_MULTIPLE_OF_BLOCKSIZE, 0};
@@ -708,43 +732,169 @@ void seg_decrypt_prepare(const rc_cipher* c, Seg& g, SegBatch& b) {
     g.err = {RC_ERR_TOO_LONG_AFTER_DECODE, 0};
     return;
   }
-  g.slot = b.add(raw.data(), raw.size());
+  g.slot = (uint32_t)b.add(raw.data(), raw.size());
   g.gpu = true;
 }
 
-void seg_encrypt_finish(const rc_cipher* c, Seg& g, const SegBatch& b) {
-  if (!g.gpu) return;
-  const xs_name_desc& d = b.desc[g.slot];
-  g.out = encode(c->name_enc, b.get(g.slot), (size_t)d.nblk * kNameBlock);
+// Phase A for input k of the chunk: resolve directly (mode "off", directory names left alone)
+// or split into segments, strip the last segment's version, and prepare every segment.
+void prepare_input(const Ctx& x, Chunk& ch, const char* s, size_t n) {
+  const rc_cipher* c = x.c;
+  ch.seg0.push_back((uint32_t)ch.segs.size());
+  uint8_t direct = 0;
+  Err derr;
+  size_t res_at = ch.res.size();
+  switch (x.op) {
+    case RC_OP_ENCRYPT_FILE_NAME:
+      if (c->mode == RC_NAME_OFF) {  // EncryptFileName :542-547
+        direct = 1;
+        ch.res.append(s, n);
+        ch.res += c->encrypted_suffix;
+      }
+      break;
+    case RC_OP_ENCRYPT_DIR_NAME:
+    case RC_OP_DECRYPT_DIR_NAME:
+      if (c->mode == RC_NAME_OFF || !c->dir_name_encrypt) {  // :550-555, :613-618
+        direct = 1;
+        ch.res.append(s, n);
+      }
+      break;
+    case RC_OP_DECRYPT_FILE_NAME:
+      if (c->mode == RC_NAME_OFF) {  // DecryptFileName :600-611
+        direct = 1;
+        const std::string& suf = c->encrypted_suffix;
+        size_t sl = suf.size();
+        bool has = n >= sl && memcmp(s + n - sl, suf.data(), sl) == 0;
+        if (n == sl || !has) {
+          derr = {RC_ERR_NOT_AN_ENCRYPTED_FILE, 0};
+        } else {
+          size_t dn = n - sl, at;
+          if (version_match(s, dn) && version_remove(s, dn, &at) && dn - kVersionLen == 0)
+            derr = {RC_ERR_NOT_AN_ENCRYPTED_FILE, 0};  // only a version left
+          else
+            ch.res.append(s, dn);
+        }
+      }
+      break;
+    default:
+      break;
+  }
+  if (direct) {
+    ch.direct.push_back(1);
+    ch.roff.push_back(res_at);
+    ch.rlen.push_back((uint32_t)(ch.res.size() - res_at));
+    ch.err.push_back(derr);
+    return;
+  }
+  ch.direct.push_back(0);
+  ch.roff.push_back(0);
+  ch.rlen.push_back(0);
+  ch.err.push_back(Err{});
+  const bool whole = x.op >= RC_OP_ENCRYPT_SEGMENT;  // segment-level ops: the input is one segment
+  size_t st = 0;
+  for (;;) {
+    size_t e = whole ? n : st;
+    if (!whole)
+      while (e < n && s[e] != '/') e++;
+    Seg g;
+    g.off = (uint32_t)st;
+    g.len = (uint32_t)(e - st);
+    bool last = e >= n;
+    g.process = whole || c->dir_name_encrypt || last;
+    const char* text = s + st;
+    if (g.process && last && !whole) {  // encryptFileName / decryptFileName strip the version (:496-507)
+      size_t at;
+      if (version_match(text, g.len) && version_remove(text, g.len, &at)) {
+        g.has_ver = true;
+        g.ver = (uint32_t)(st + at);
+        size_t o = ch.own.size();
+        ch.own.append(text, at);
+        ch.own.append(text + at + kVersionLen, g.len - at - kVersionLen);
+        g.owned = true;
+        g.off = (uint32_t)o;
+        g.len -= (uint32_t)kVersionLen;
+      }
+    }
+    if (g.process) {
+      const char* t = g.owned ? ch.own.data() + g.off : s + g.off;
+      if (x.standard) {
+        if (g.len == 0) {
+          // encryptSegment("") == decryptSegment("") == "" (cipher.go:281, :294)
+        } else if (x.enc_dir)
+          seg_encrypt_prepare(g, t, ch.batch);
+        else
+          seg_decrypt_prepare(c, g, t, ch.batch);
+      } else {
+        std::string in(t, g.len), out;
+        if (x.enc_dir)
+          out = obfuscate(c, in);
+        else
+          g.err = deobfuscate(c, in, &out);
+        g.out_off = (uint32_t)ch.segout.size();
+        g.out_len = (uint32_t)out.size();
+        ch.segout += out;
+      }
+    }
+    ch.segs.push_back(g);
+    if (last) break;
+    st = e + 1;
+  }
 }
 
-// pkcs7.Unpad(16, ...) after the kernel
-void seg_decrypt_finish(Seg& g, const SegBatch& b) {
-  if (!g.gpu) return;
-  const uint8_t* p = b.get(g.slot);
-  size_t len = (size_t)b.desc[g.slot].nblk * kNameBlock;
-  int pad = p[len - 1];
-  if (pad > kNameBlock) {
-    g.err = {RC_ERR_PKCS7_TOO_LONG, 0};
-    return;
-  }
-  if (pad == 0) {
-    g.err = {RC_ERR_PKCS7_TOO_SHORT, 0};
-    return;
-  }
-  for (int i = 0; i < pad; i++)
-    if (p[len - 1 - i] != pad) {
-      g.err = {RC_ERR_PKCS7_NOT_ALL_THE_SAME, 0};
-      return;
+// Phase C for input k: encode / unpad each segment, first error wins, reassemble with '/'.
+void finish_input(const Ctx& x, Chunk& ch, size_t k, const char* s) {
+  if (ch.direct[k]) return;
+  const rc_cipher* c = x.c;
+  size_t start = ch.res.size();
+  Err first;
+  uint32_t e = k + 1 < ch.seg0.size() ? ch.seg0[k + 1] : (uint32_t)ch.segs.size();
+  for (uint32_t q = ch.seg0[k]; q < e; q++) {
+    Seg& g = ch.segs[q];
+    if (q != ch.seg0[k]) ch.res += '/';
+    size_t at = ch.res.size();
+    if (!g.process) {
+      ch.res.append(s + g.off, g.len);
+      continue;
     }
-  g.out.assign((const char*)p, len - pad);
+    if (g.err.code == RC_NIL && g.gpu) {
+      const uint8_t* p = ch.batch.get(g.slot);
+      size_t len = (size_t)ch.batch.desc[g.slot].nblk * kNameBlock;
+      if (x.enc_dir) {
+        encode_append(c->name_enc, p, len, ch.res);
+      } else {  // pkcs7.Unpad(16)
+        int pad = p[len - 1];
+        if (pad > kNameBlock) {
+          g.err = {RC_ERR_PKCS7_TOO_LONG, 0};
+        } else if (pad == 0) {
+          g.err = {RC_ERR_PKCS7_TOO_SHORT, 0};
+        } else {
+          for (int i = 0; i < pad; i++)
+            if (p[len - 1 - i] != pad) {
+              g.err = {RC_ERR_PKCS7_NOT_ALL_THE_SAME, 0};
+              break;
+            }
+        }
+        if (g.err.code == RC_NIL) ch.res.append((const char*)p, len - pad);
+      }
+    } else if (g.err.code == RC_NIL) {
+      ch.res.append(ch.segout, g.out_off, g.out_len);
+    }
+    if (g.err.code != RC_NIL) {  // decryptFileName returns at the first failing segment
+      first = g.err;
+      break;
+    }
+    if (g.has_ver) version_add_at(ch.res, at, s + g.ver);
+  }
+  if (first.code != RC_NIL) ch.res.resize(start);
+  ch.roff[k] = start;
+  ch.rlen[k] = (uint32_t)(ch.res.size() - start);
+  ch.err[k] = first;
 }
 
 }  // namespace
 
 struct rc_names {
-  std::vector<std::string> s;
-  std::vector<Err> err;
+  std::vector<Chunk> chunks;
   double kernel_ms = 0;
 };
 
@@ -798,7 +948,7 @@ int64_t rc_name_encode(int32_t enc, const uint8_t* src, uint64_t n, char* out, u
 int32_t rc_name_decode(int32_t enc, const char* s, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len,
                        int64_t* err_arg) {
   std::vector<uint8_t> v;
-  Err e = decode(enc, std::string(s ? s : "", n), v);
+  Err e = decode(enc, s ? s : "", s ? n : 0, v);
   if (out) memcpy(out, v.data(), v.size() < cap ? v.size() : cap);
   if (out_len) *out_len = v.size();
   if (err_arg) *err_arg = e.arg;
@@ -826,143 +976,56 @@ int32_t rc_names_run(rc_cipher* c, int32_t op, uint64_t n, const char* const* in
                      rc_names** out) {
   if (!c || !out || (n && (!in || !in_len)) || op < 0 || op > RC_OP_DEOBFUSCATE_SEGMENT) return RC_ERR_INVALID;
   *out = nullptr;
-  const bool enc_dir = op == RC_OP_ENCRYPT_FILE_NAME || op == RC_OP_ENCRYPT_DIR_NAME || op == RC_OP_ENCRYPT_SEGMENT ||
-                       op == RC_OP_OBFUSCATE_SEGMENT;
-  std::vector<Job> jobs(n);
-  SegBatch batch;
-  for (uint64_t i = 0; i < n; i++) {
-    std::string s(in[i] ? in[i] : "", in_len[i]);
-    Job& j = jobs[i];
-    switch (op) {
-      case RC_OP_ENCRYPT_SEGMENT:
-      case RC_OP_DECRYPT_SEGMENT:
-      case RC_OP_OBFUSCATE_SEGMENT:
-      case RC_OP_DEOBFUSCATE_SEGMENT: {
-        Seg g;
-        g.text = s;
-        g.process = true;
-        j.segs.push_back(std::move(g));
-        break;
-      }
-      case RC_OP_ENCRYPT_FILE_NAME:
-        if (c->mode == RC_NAME_OFF) {  // EncryptFileName :542-547
-          j.direct = true;
-          j.out = s + c->encrypted_suffix;
-        }
-        break;
-      case RC_OP_ENCRYPT_DIR_NAME:
-      case RC_OP_DECRYPT_DIR_NAME:
-        if (c->mode == RC_NAME_OFF || !c->dir_name_encrypt) {  // :550-555, :613-618
-          j.direct = true;
-          j.out = s;
-        }
-        break;
-      case RC_OP_DECRYPT_FILE_NAME:
-        if (c->mode == RC_NAME_OFF) {  // DecryptFileName :600-611
-          j.direct = true;
-          size_t sl = c->encrypted_suffix.size();
-          bool has = s.size() >= sl && s.compare(s.size() - sl, sl, c->encrypted_suffix) == 0;
-          if (s.size() == sl || !has) {
-            j.err = {RC_ERR_NOT_AN_ENCRYPTED_FILE, 0};
-          } else {
-            std::string dec = s.substr(0, s.size() - sl);
-            std::string stripped, ver;
-            if (version_match(dec)) {
-              if (!version_remove(dec, &stripped, &ver)) stripped = dec;
-              if (stripped.empty()) j.err = {RC_ERR_NOT_AN_ENCRYPTED_FILE, 0};
-            }
-            if (j.err.code == RC_NIL) j.out = dec;
-          }
-        }
-        break;
-    }
-    if (j.direct || !j.segs.empty()) continue;
-    // encryptFileName / decryptFileName (:482-539, :558-598)
-    std::vector<std::string> parts = split_path(s);
-    j.segs.resize(parts.size());
-    for (size_t k = 0; k < parts.size(); k++) {
-      Seg& g = j.segs[k];
-      g.text = parts[k];
-      bool last = k + 1 == parts.size();
-      g.process = c->dir_name_encrypt || last;
-      if (!g.process) continue;
-      if (last && version_match(g.text)) {
-        std::string stripped, ver;
-        if (version_remove(g.text, &stripped, &ver) && stripped != g.text) {
-          g.text = stripped;
-          g.ver = ver;
-          g.has_ver = true;
-        }
-      }
-    }
-  }
-  // host half before the kernel
-  const bool standard = op == RC_OP_ENCRYPT_SEGMENT || op == RC_OP_DECRYPT_SEGMENT ||
-                        ((op == RC_OP_ENCRYPT_FILE_NAME || op == RC_OP_DECRYPT_FILE_NAME || op == RC_OP_ENCRYPT_DIR_NAME ||
-                          op == RC_OP_DECRYPT_DIR_NAME) &&
-                         c->mode == RC_NAME_STANDARD);
-  for (auto& j : jobs) {
-    if (j.direct) continue;
-    for (auto& g : j.segs) {
-      if (!g.process) continue;
-      if (standard) {
-        if (enc_dir)
-          seg_encrypt_prepare(g, batch);
-        else
-          seg_decrypt_prepare(c, g, batch);
-      } else if (enc_dir) {
-        g.out = obfuscate(c, g.text);
-      } else {
-        g.err = deobfuscate(c, g.text, &g.out);
-      }
-    }
-  }
+  for (uint64_t i = 0; i < n; i++)
+    if (in_len[i] > 0xFFFFFFF0u || (in_len[i] && !in[i])) return RC_ERR_INVALID;
+  Ctx x;
+  x.c = c;
+  x.op = op;
+  x.enc_dir = op == RC_OP_ENCRYPT_FILE_NAME || op == RC_OP_ENCRYPT_DIR_NAME || op == RC_OP_ENCRYPT_SEGMENT ||
+              op == RC_OP_OBFUSCATE_SEGMENT;
+  x.standard = op == RC_OP_ENCRYPT_SEGMENT || op == RC_OP_DECRYPT_SEGMENT ||
+               (op <= RC_OP_DECRYPT_DIR_NAME && c->mode == RC_NAME_STANDARD);
   rc_names* r = new rc_names();
-  int32_t rc = run_eme(c, enc_dir, batch, &r->kernel_ms);
+  const size_t nchunks = (n + kChunkNames - 1) / kChunkNames;
+  r->chunks.resize(nchunks);
+  // host half before the kernel: split, strip versions, pad / decode, pack
+  parallel_for(nchunks, [&](size_t ci) {
+    Chunk& ch = r->chunks[ci];
+    uint64_t i0 = ci * kChunkNames, i1 = std::min<uint64_t>(n, i0 + kChunkNames);
+    ch.segs.reserve(i1 - i0);
+    ch.batch.data.reserve((i1 - i0) * 48);
+    for (uint64_t i = i0; i < i1; i++) prepare_input(x, ch, in[i], in_len[i]);
+  });
+  std::vector<SegBatch*> parts(nchunks);
+  for (size_t ci = 0; ci < nchunks; ci++) parts[ci] = &r->chunks[ci].batch;
+  int32_t rc = run_eme(c, x.enc_dir, parts, &r->kernel_ms);
   if (rc != RC_NIL) {
     delete r;
     return rc;
   }
-  r->s.resize(n);
-  r->err.resize(n);
-  for (uint64_t i = 0; i < n; i++) {
-    Job& j = jobs[i];
-    if (j.direct) {
-      r->err[i] = j.err;
-      if (j.err.code == RC_NIL) r->s[i] = std::move(j.out);
-      continue;
-    }
-    std::string res;
-    Err first;
-    for (size_t k = 0; k < j.segs.size(); k++) {
-      Seg& g = j.segs[k];
-      if (g.process && g.gpu) {
-        if (enc_dir)
-          seg_encrypt_finish(c, g, batch);
-        else
-          seg_decrypt_finish(g, batch);
-      }
-      if (g.process && g.err.code != RC_NIL) {  // the first failing segment's error wins
-        first = g.err;
-        break;
-      }
-      std::string piece = g.process ? g.out : g.text;
-      if (g.has_ver) piece = version_add(piece, g.ver);
-      if (k) res += '/';
-      res += piece;
-    }
-    r->err[i] = first;
-    if (first.code == RC_NIL) r->s[i] = std::move(res);
-  }
+  // host half after the kernel: encode / unpad, first error per name, reassemble
+  parallel_for(nchunks, [&](size_t ci) {
+    Chunk& ch = r->chunks[ci];
+    uint64_t i0 = ci * kChunkNames, i1 = std::min<uint64_t>(n, i0 + kChunkNames);
+    ch.res.reserve(ch.res.size() + ch.batch.data.size() * 2 + (i1 - i0) * 8);
+    for (uint64_t i = i0; i < i1; i++) finish_input(x, ch, i - i0, in[i]);
+    std::vector<Seg>().swap(ch.segs);
+    std::vector<uint32_t>().swap(ch.seg0);
+    std::string().swap(ch.own);
+    std::string().swap(ch.segout);
+    ch.batch = SegBatch();
+  });
   *out = r;
   return RC_NIL;
 }
 
 void rc_names_get(const rc_names* r, uint64_t i, const char** s, uint64_t* len, int32_t* err, int64_t* err_arg) {
-  if (s) *s = r->s[i].data();
-  if (len) *len = r->s[i].size();
-  if (err) *err = r->err[i].code;
-  if (err_arg) *err_arg = r->err[i].arg;
+  const Chunk& ch = r->chunks[i / kChunkNames];
+  uint64_t k = i % kChunkNames;
+  if (s) *s = ch.res.data() + ch.roff[k];
+  if (len) *len = ch.rlen[k];
+  if (err) *err = ch.err[k].code;
+  if (err_arg) *err_arg = ch.err[k].arg;
 }
 
 double rc_names_kernel_ms(const rc_names* r) { return r->kernel_ms; }

@@ -238,3 +238,21 @@ def test_version_strip_only_valid_dates():
     bad = c.encrypt_file_name("a-v2023-02-29-235959-999.txt")  # no Feb 29 in 2023: not a version
     assert "-v2023" not in bad
     assert c.decrypt_file_name(bad) == "a-v2023-02-29-235959-999.txt"
+
+
+def test_multi_chunk_batches_match_single_calls():
+    # > 8192 inputs span several host chunks (and threads): results keep their order and equal
+    # the one-name calls; mode "off" and obfuscation need no device
+    import random
+    rng = random.Random(21)
+    c = _c(names.NAME_ENCRYPTION_OBFUSCATED, False)
+    paths = ["d%d/e%d/f%05d-v2001-02-03-040506-123.txt" % (i % 7, i % 11, i) if i % 3 == 0 else
+             "".join(rng.choice("aZ09!é中") for _ in range(rng.randrange(1, 12))) for i in range(20000)]
+    enc = c.encrypt_file_names(paths)
+    for i in range(0, 20000, 997):
+        assert enc[i] == c.encrypt_file_name(paths[i])
+    assert c.decrypt_file_names(enc) == paths
+    off = _c(names.NAME_ENCRYPTION_OFF)
+    got = off.decrypt_file_names([p + ".bin" for p in paths[:9000]] + ["x.bix", ".bin"])
+    assert got[:9000] == paths[:9000]
+    assert got[9000] == names.ErrorNotAnEncryptedFile() and got[9001] == names.ErrorNotAnEncryptedFile()

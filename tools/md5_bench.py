@@ -2,8 +2,8 @@
 """GPU MD5 of crypt files (one lane per object) vs the host: device-resident kernel rate for
 N objects of one sealed 64 KiB block each (65 584-byte crypt files), and the end-to-end
 batched cryptcheck call (host plaintext -> GPU seal -> GPU MD5 -> 16 B/object back) for
-BASELINE configs[0]'s 1000 x 64 KiB.  CPU reference: hashlib.md5 on one core, and the oracle
-seal + hashlib for the same 1000 objects."""
+BASELINE configs[0]'s 1000 x 64 KiB.  CPU reference: hashlib.md5 on one core.  (The oracle is
+test infrastructure and is not used here; the digests' parity is tests/test_md5_gpu.py.)"""
 import hashlib
 import json
 import os
@@ -64,13 +64,6 @@ def main():
     got = c.hash_batch_with_nonce([(nonces[i], Buffer(plains[i])) for i in range(1000)])
     el = time.perf_counter() - t0
     res["cryptcheck_1000x64KiB_gpu"] = {"s": round(el, 4), "GiB_s": round(1000 * 65536 / 2**30 / el, 3)}
-    from oracle import pyoracle as orc
-    key = c.data_key
-    t0 = time.perf_counter()
-    ref = [hashlib.md5(orc.encrypt_file(plains[i], nonces[i], key)).digest() for i in range(1000)]
-    el = time.perf_counter() - t0
-    res["cryptcheck_1000x64KiB_cpu_1core"] = {"s": round(el, 4), "GiB_s": round(1000 * 65536 / 2**30 / el, 3)}
-    res["match"] = got == ref
     print(json.dumps(res))
 
 
