@@ -144,7 +144,9 @@ static const uint8_t kMagic[8] = {'R', 'C', 'L', 'O', 'N', 'E', 0, 0};
 
 // memory remote (backend/memory): objects keep header + body bytes and a lazily cached MD5
 struct Obj {
-  std::string name;
+  std::string name;          // local file
+  std::string rel;           // path relative to the synced root (what crypt encrypts)
+  std::string remote;        // EncryptFileName(rel): the object's key on the wrapped remote
   uint64_t size = 0;         // plaintext size (local file)
   uint8_t header[32];        // magic || nonce
   uint8_t* body = nullptr;   // wire body in the arena
@@ -202,6 +204,33 @@ static int64_t mem_read(void* u, uint8_t* p, int64_t n, int32_t* err) {
 }
 static int32_t mem_close(void*) { return RC_NIL; }
 
+static const int kSubdirs = 64;
+
+// EncryptFileName / DecryptFileName for every object in one batch (rc_names_run: one EME launch)
+static bool names_batch(rc_cipher* c, int32_t op, const std::vector<const std::string*>& in, std::vector<std::string>& out) {
+  std::vector<const char*> p(in.size());
+  std::vector<uint64_t> l(in.size());
+  for (size_t i = 0; i < in.size(); i++) {
+    p[i] = in[i]->data();
+    l[i] = in[i]->size();
+  }
+  rc_names* r = nullptr;
+  if (rc_names_run(c, op, in.size(), p.data(), l.data(), &r) != RC_NIL) return false;
+  out.resize(in.size());
+  bool ok = true;
+  for (size_t i = 0; i < in.size(); i++) {
+    const char* s;
+    uint64_t n;
+    int32_t e;
+    int64_t a;
+    rc_names_get(r, i, &s, &n, &e, &a);
+    if (e != RC_NIL) ok = false;
+    out[i].assign(s, n);
+  }
+  rc_names_free(r);
+  return ok;
+}
+
 int main(int argc, char** argv) {
   double gib = 8.0;
   std::string dir = "/tmp/rc_e2e_src", mode = "batch";
@@ -243,9 +272,13 @@ int main(int argc, char** argv) {
       total += o.size;
       objs.push_back(o);
     }
-    for (size_t i = 0; i < objs.size(); i++) objs[i].name = dir + "/f" + std::to_string(i);
+    for (size_t i = 0; i < objs.size(); i++) {
+      objs[i].rel = "d" + std::to_string(i % kSubdirs) + "/f" + std::to_string(i) + ".dat";
+      objs[i].name = dir + "/" + objs[i].rel;
+    }
   }
   mkdir(dir.c_str(), 0755);
+  for (int d = 0; d < kSubdirs; d++) mkdir((dir + "/d" + std::to_string(d)).c_str(), 0755);
   uint64_t total = 0;
   for (auto& o : objs) total += o.size;
   const double tg0 = now();
@@ -352,8 +385,17 @@ int main(int argc, char** argv) {
     for (auto& t : th) t.join();
   };
   // ---- sync
-  double t_sync = 0, t_dst = 0, sync_read = 0, sync_gpu = 0;
-  uint64_t put_mismatch = 0;
+  double t_sync = 0, t_dst = 0, sync_read = 0, sync_gpu = 0, t_names_enc = 0, t_names_dec = 0;
+  uint64_t put_mismatch = 0, name_mismatch = 0;
+  const double tn0 = now();
+  {  // crypt.Put's remote name: EncryptFileName(rel) for the whole listing (crypt.go:517)
+    std::vector<const std::string*> in(objs.size());
+    std::vector<std::string> out;
+    for (size_t i = 0; i < objs.size(); i++) in[i] = &objs[i].rel;
+    if (!names_batch(c, RC_OP_ENCRYPT_FILE_NAME, in, out)) failures++;
+    for (size_t i = 0; i < objs.size() && i < out.size(); i++) objs[i].remote = std::move(out[i]);
+  }
+  t_names_enc = now() - tn0;
   if (mode == "batch") {
     const double t0 = now();
     run_groups([&](int l, size_t g, const std::vector<uint64_t>& offs) {
@@ -367,7 +409,7 @@ int main(int argc, char** argv) {
       }
       for (size_t k = 0; k < n; k++) memcpy(objs[a + k].tee, md5.data() + 16 * k, 16);
     });
-    t_sync = now() - t0;
+    t_sync = now() - t0 + t_names_enc;
     sync_read = t_read;
     sync_gpu = t_gpu;
   } else {
@@ -405,7 +447,7 @@ int main(int argc, char** argv) {
       memcpy(o.body, ct.data() + 32, o.body_len);
       fd_close(&fr);
     });
-    t_sync = now() - t0;
+    t_sync = now() - t0 + t_names_enc;
   }
   if (check_dst) {  // crypt.put: srcHash (tee) vs dstHash (the remote's MD5 of what it stored)
     const double t0 = now();
@@ -438,6 +480,14 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> differ;
   t_read = t_gpu = 0;
   const double tc0 = now();
+  {  // cryptcheck lists crypt: -> DecryptFileName of every remote key, matched to the source paths
+    std::vector<const std::string*> in(objs.size());
+    std::vector<std::string> out;
+    for (size_t i = 0; i < objs.size(); i++) in[i] = &objs[i].remote;
+    if (!names_batch(c, RC_OP_DECRYPT_FILE_NAME, in, out)) failures++;
+    for (size_t i = 0; i < objs.size() && i < out.size(); i++) name_mismatch += out[i] != objs[i].rel;
+  }
+  t_names_dec = now() - tc0;
   cryptcheck(differ);
   const double t_check = now() - tc0, check_read = t_read, check_gpu = t_gpu;
   uint64_t ndiff = 0;
@@ -479,19 +529,22 @@ int main(int argc, char** argv) {
     for (auto d : d2) flagged += d;
     only_victim = flagged == 1 && d2[victim];
   }
-  const bool ok = failures == 0 && put_mismatch == 0 && ndiff == 0 && verify_bad == 0 && only_victim;
+  const bool ok = failures == 0 && put_mismatch == 0 && ndiff == 0 && verify_bad == 0 && only_victim && name_mismatch == 0;
   const double g = (double)total / 1073741824.0;
   printf("{\"config\": \"configs[4] e2e: sync local tree -> crypt(memory), cryptcheck\", \"mode\": \"%s\", "
          "\"objects\": %zu, \"gib\": %.3f, \"transfers\": %d, \"lanes\": %d, \"group_mib\": %llu, "
          "\"sync_s\": %.3f, \"sync_GiB_s\": %.2f, \"dst_hash_s\": %.3f, \"sync_with_hash_check_GiB_s\": %.2f, "
          "\"cryptcheck_s\": %.3f, \"cryptcheck_GiB_s\": %.2f, \"put_hash_mismatches\": %llu, "
          "\"cryptcheck_differences\": %llu, \"verified_objects\": %llu, \"verify_failures\": %llu, "
-         "\"corruption_flagged\": %llu, \"tree_write_s\": %.2f, \"lane_seconds\": {\"sync_read\": %.3f, "
+         "\"corruption_flagged\": %llu, \"names_encrypt_s\": %.4f, \"names_decrypt_s\": %.4f, "
+         "\"name_mismatches\": %llu, \"example_remote_name\": \"%s\", "
+         "\"tree_write_s\": %.2f, \"lane_seconds\": {\"sync_read\": %.3f, "
          "\"sync_gpu\": %.3f, \"check_read\": %.3f, \"check_gpu\": %.3f}, \"ok\": %s}\n",
          mode.c_str(), objs.size(), g, transfers, lanes, (unsigned long long)group_mib, t_sync, g / t_sync, t_dst,
          check_dst ? g / (t_sync + t_dst) : 0.0, t_check, g / t_check, (unsigned long long)put_mismatch,
          (unsigned long long)ndiff, (unsigned long long)verified, (unsigned long long)verify_bad,
-         (unsigned long long)flagged, t_gen, sync_read, sync_gpu, check_read, check_gpu, ok ? "true" : "false");
+         (unsigned long long)flagged, t_names_enc, t_names_dec, (unsigned long long)name_mismatch,
+         objs.empty() ? "" : objs.back().remote.c_str(), t_gen, sync_read, sync_gpu, check_read, check_gpu, ok ? "true" : "false");
   for (int l = 0; l < lanes; l++) {
     xs_engine_destroy(eng[l]);
     xs_host_free(stage[l]);
@@ -500,6 +553,7 @@ int main(int argc, char** argv) {
   rc_cipher_free(c);
   if (!keep) {
     for (auto& o : objs) unlink(o.name.c_str());
+    for (int d = 0; d < kSubdirs; d++) rmdir((dir + "/d" + std::to_string(d)).c_str());
     rmdir(dir.c_str());
   }
   return ok ? 0 : 1;
