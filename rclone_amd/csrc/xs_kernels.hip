@@ -13,16 +13,20 @@
 //              Salsa20 keystream blocks K = l + 64*s (s = 0..15), i.e. message chunks
 //              4K-2 .. 4K+1 (16 bytes each, offset by the 32-byte Poly1305 key).  A lane
 //              keeps the whole 16-word Salsa20 state in VGPRs; key/nonce words are
-//              wave-uniform and live in SGPRs.  Each lane runs a strided Horner over its
-//              own chunks with uniform multipliers r (inside a group) and r^253 (between
-//              groups), then multiplies by r^e (e = chunks after its last one) from the
-//              tables; the 64 partial sums are added with wave shuffles and lane 0 adds s
-//              and writes (seal) or checks (open) the tag.
+//              wave-uniform and live in SGPRs.  Each 4 KiB group is staged through LDS with
+//              1 KiB-contiguous loads and stores.  Poly1305 of a full block runs on the
+//              matrix cores (crypt_block_mfma): the chunk sums against the powers r^(64k)
+//              are an i8 GEMM on v_mfma_i32_16x16x64_i8 whose B operand is each lane's own
+//              ciphertext; one transpose at the end gives each lane one column to fold and
+//              multiply by r^(66-g).  Partial blocks run a strided VALU Horner (uniform
+//              multipliers r inside a group, r^253 between groups, final r^e from the
+//              tables; the 64 partial sums added with wave shuffles).  Lane 0 adds s and
+//              writes (seal) or checks (open) the tag.
 //   Poly1305 arithmetic is radix 2^26 (5 limbs): the product columns are
 //   v_mad_u64_u32 chains, which measured as fast as v_alignbit on gfx950.
 //
-// There is no MFMA here: the work is 32-bit add/rotate/xor (Salsa20) and 32x32->64
-// multiply-add (Poly1305) on the VALU, plus one HBM read and one HBM write per byte.
+// The bound is the VALU issue rate (Salsa20 add/rotate/xor, ~90% of the instructions) at the
+// power-limited clock, plus one HBM read and one HBM write per byte.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
