@@ -282,7 +282,7 @@ def run_names(args, world, rank):
     el = time.perf_counter() - t0
     if world > 1:
         import torch.distributed as dist
-        t = torch.tensor([el], dtype=torch.float64)
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")  # RCCL reduces device tensors only
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     if rank == 0:
@@ -307,6 +307,9 @@ def run_names(args, world, rank):
         if not args.no_cpu:
             res["cpu_baseline"] = names_cpu_baseline(segs, c.name_key, c.name_tweak, 5.0)
         print(json.dumps(res), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 def main():
@@ -317,10 +320,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BENCH_DIST_BACKEND=gloo rehearses the N>1 path on a box with fewer GPUs than ranks (ranks
+    # share GPUs round-robin; counters and times go through gloo).  The real run is RCCL, one
+    # rank per GPU.
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    gpu = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
+    # the C library's engines (rc_* handles, file names) run on this rank's GPU too
+    os.environ.setdefault("RCLONE_AMD_DEVICE", str(gpu))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     if args.object_blocks:
