@@ -51,6 +51,10 @@ def parse():
                     help="configs[3] mode: one logical object of this many blocks (2^24 = 1 TiB) split "
                          "round-robin over the ranks, processed in --blocks rounds with on-device "
                          "generation inside each step (0 = the default resident-set bench)")
+    ap.add_argument("--mixed-gib", type=float, default=0.0,
+                    help="configs[2] mode: this many GiB of 4 KiB-8 MiB objects per rank (descriptor batches, "
+                         "partial last blocks, ~0.1%% of the blocks tampered); one step = seal the set + "
+                         "open+verify its tampered wire image (0 = the default resident-set bench)")
     ap.add_argument("--names", type=int, default=0,
                     help="file-name mode (SURVEY 8(f) rank 4): encrypt + decrypt this many names per step "
                          "through rc_names_run (0 = the default crypt-block bench)")
@@ -183,6 +187,162 @@ def run_objectset(args, world, rank, dev, dist):
             "counters": {"blocks": blocks, "bytes": nbytes, "tag_failures": fails, "roundtrip_mismatch_rounds": mism,
                          "tag_digest": f"{d1:016x}{d0:016x}"},
             "roofline": None, "cpu_baseline": None,
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_mixed(args, world, rank, dev, dist):
+    """BASELINE configs[2]: decrypt+verify of mixed 4 KiB-8 MiB objects chunked to 64 KiB, with
+    tag-fail injection.  Each rank owns its own object set (weak scaling).  The set is sealed on
+    the GPU once (sampled blocks checked against the oracle on rank 0), ~0.1% of its blocks get
+    one byte flipped (tag bytes, first / last / random ciphertext byte), then one step = seal the
+    plaintext image into a second wire image + open+verify the tampered one, each as one
+    descriptor batch (keygen + block kernel).  After the timed steps the failing set must be
+    exactly the tampered blocks, zero-filled, and every other byte equal to the plaintext."""
+    import numpy as np
+    import torch
+
+    from rclone_amd import _lib, device, shard
+    L = _lib.lib()
+    seed = 0xC0F3 + rank
+    rng = np.random.default_rng(seed)
+    key = bytes(32)  # crypt with an empty password: all-zero data key (cipher.go:231-236)
+    sizes, nonces, pstart, wstart, ptot, wtot, d, obj = shard.mixed_object_layout(int(args.mixed_gib * 2**30), rng)
+    nb = len(d)
+    od = d.copy()
+    od["src"], od["dst"] = d["dst"], d["src"]
+
+    def dev_bytes(a):
+        return torch.from_numpy(np.frombuffer(a.tobytes(), dtype=np.uint8).copy()).to(dev)
+    d_seal, d_open = dev_bytes(d), dev_bytes(od)
+    plain = torch.empty(ptot, dtype=torch.uint8, device=dev)
+    device.fill_random(plain, seed)
+    for o, sz in enumerate(sizes):  # alignment gaps are never written by open: keep them zero
+        end = pstart[o] + sz
+        nxt = pstart[o + 1] if o + 1 < len(sizes) else ptot
+        if nxt > end:
+            plain[end:nxt] = 0
+    wire_a = torch.zeros(wtot, dtype=torch.uint8, device=dev)
+    wire_b = torch.zeros(wtot, dtype=torch.uint8, device=dev)
+    out = torch.zeros(ptot, dtype=torch.uint8, device=dev)
+    ok = torch.empty(nb, dtype=torch.uint8, device=dev)
+    ws_seal = device.workspace(nb, dev)
+    ws_open = device.workspace(nb, dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+
+    def seal(dst, ev=None):
+        _lib.check(L.xs_keygen_batch_dev(1, key, d_seal.data_ptr(), nb, plain.data_ptr(), ptot, dst.data_ptr(),
+                                         wtot, ws_seal.data_ptr(), sp), "keygen")
+        if ev is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+        _lib.check(L.xs_crypt_dev(1, ws_seal.data_ptr(), nb, plain.data_ptr(), dst.data_ptr(), None, sp), "seal")
+        if ev is not None:
+            b.record(stream)
+            ev.append((True, a, b))
+
+    def open_(ev=None):
+        _lib.check(L.xs_keygen_batch_dev(0, key, d_open.data_ptr(), nb, wire_a.data_ptr(), wtot, out.data_ptr(),
+                                         ptot, ws_open.data_ptr(), sp), "keygen")
+        if ev is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+        _lib.check(L.xs_crypt_dev(0, ws_open.data_ptr(), nb, wire_a.data_ptr(), out.data_ptr(), ok.data_ptr(), sp),
+                   "open")
+        if ev is not None:
+            b.record(stream)
+            ev.append((False, a, b))
+
+    seal(wire_a)
+    torch.cuda.synchronize(dev)
+    if rank == 0 and not args.no_cpu:  # the oracle checks sampled blocks (never timed)
+        from oracle import pyoracle as orc
+        partial = int(np.flatnonzero(d["len"] < BLOCK_DATA)[0])
+        carry = int(np.flatnonzero(obj == 0)[-1])  # object 0's nonce carries out of byte 7
+        for i in sorted({0, partial, carry, nb // 2, nb - 1}):
+            s0, w0, n = int(d["src"][i]), int(d["dst"][i]), int(d["len"][i])
+            p = plain[s0:s0 + n].cpu().numpy().tobytes()
+            w = wire_a[w0:w0 + 16 + n].cpu().numpy().tobytes()
+            if orc.seal(p, bytes(d["nonce"][i]), key) != w:
+                raise SystemExit("bench: mixed block %d differs from the oracle" % i)
+    nbad = max(3, nb // 1000)
+    bad = np.sort(rng.choice(nb, nbad, replace=False))
+    pos = []
+    for j, b in enumerate(bad.tolist()):
+        blen = 16 + int(d["len"][b])
+        pos.append(int(d["dst"][b]) + [0, 15, 16, blen - 1, int(rng.integers(0, blen))][j % 5])
+    idx = torch.tensor(pos, dtype=torch.int64, device=dev)
+    wire_a[idx] ^= 0x40
+    for _ in range(args.warmup):
+        seal(wire_b)
+        open_()
+    torch.cuda.synchronize(dev)
+    ev = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        seal(wire_b, ev)
+        open_(ev)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    # verification after the timed region: exactly the tampered blocks fail, are zero-filled, the
+    # rest is the plaintext; the second wire image equals the first away from the flipped bytes
+    fails = np.flatnonzero(ok.cpu().numpy() == 0)
+    expect = plain.clone()
+    for b in bad.tolist():
+        s0, n = int(d["src"][b]), int(d["len"][b])
+        expect[s0:s0 + n] = 0
+    wire_b[idx] ^= 0x40
+    good = np.array_equal(fails, bad) and bool(torch.equal(out, expect)) and bool(torch.equal(wire_a, wire_b))
+    del expect
+    counters = torch.tensor([args.steps * 2 * nb, args.steps * 2 * int(d["len"].sum()), len(fails),
+                             0 if good else 1], dtype=torch.int64, device=dev)
+    tmax = torch.tensor([el], dtype=torch.float64, device=dev)
+    shard.reduce_counters(counters, dist if world > 1 else None)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    el = float(tmax.item())
+    if int(counters[3].item()):
+        raise SystemExit("bench: mixed object set verification failed")
+    seal_ms = [a.elapsed_time(b) for s_, a, b in ev if s_]
+    open_ms = [a.elapsed_time(b) for s_, a, b in ev if not s_]
+    seal_avg, open_avg = sum(seal_ms) / len(seal_ms), sum(open_ms) / len(open_ms)
+    plain_bytes = int(d["len"].sum())
+    alg_seal = 2 * plain_bytes + 16 * nb          # read len, write 16 + len per block
+    alg_open = 2 * plain_bytes + 16 * nb + nb     # read 16 + len, write len + 1 ok byte
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(int(counters[1].item()) / 2**30 / el, 3),
+            "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (SplitMix64 plaintext generated in HBM, seeded object sizes and nonces)",
+            "config": {"workload": f"{plain_bytes / 2**30:.2f} GiB per rank of {len(sizes)} objects, sizes "
+                                   f"log-uniform 4 KiB-8 MiB, {nb} blocks ({int((d['len'] < BLOCK_DATA).sum())} "
+                                   f"partial), {nbad} tampered; seal + open+verify as descriptor batches "
+                                   f"(BASELINE configs[2])",
+                       "objects": len(sizes), "blocks": nb, "tampered_blocks": nbad,
+                       "parallelism": f"{world} rank(s), one object set each, counters all-reduced"},
+            "seal_GiB_s": round(plain_bytes / 2**30 / (seal_avg * 1e-3), 3),
+            "open_GiB_s": round(plain_bytes / 2**30 / (open_avg * 1e-3), 3),
+            "roofline": {"bound": "hbm", "kernel": "xs_open", "achieved": round(alg_open / (open_avg * 1e-3) / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(alg_open / (open_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel_ms_avg": round(open_avg, 4), "alg_bytes_per_launch": alg_open,
+                         "seal": {"kernel": "xs_seal", "kernel_ms_avg": round(seal_avg, 4),
+                                  "achieved": round(alg_seal / (seal_avg * 1e-3) / 1e9, 1),
+                                  "frac": round(alg_seal / (seal_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}},
+            "counters": {"blocks": int(counters[0].item()), "bytes": int(counters[1].item()),
+                         "tag_failures_last_step": int(counters[2].item()), "verified": True},
+            "cpu_baseline": None,
         }
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -340,6 +500,8 @@ def main():
         return run_objectset(args, world, rank, dev, dist)
     if args.names:
         return run_names(args, world, rank)
+    if args.mixed_gib:
+        return run_mixed(args, world, rank, dev, dist)
 
     import numpy as np
 

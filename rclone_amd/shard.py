@@ -7,6 +7,8 @@ blocks through the descriptor entry point (per-block nonce = nonce0 + b), laid o
 contiguously in its own HBM.  The only collective is one all-reduce of a few int64 counters
 (blocks, bytes, tag failures) -- RCCL over xGMI with backend "nccl", gloo on CPU.
 """
+import math
+
 import numpy as np
 
 from ._lib import XsBlockDesc
@@ -59,6 +61,54 @@ def seal_descriptors(nonce0: bytes, global_idx: np.ndarray, block_len: int = BLO
     d["len"] = block_len
     d["nonce"] = nonce_plus(nonce0, global_idx)
     return d
+
+
+DESC_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("len", "<u4"), ("res", "<u4"), ("nonce", "u1", (24,))])
+
+
+def _align16(x):
+    return (x + 15) & ~15
+
+
+def mixed_object_layout(total, rng, min_size=4096, max_size=8 << 20):
+    """BASELINE configs[2] object set: sizes log-uniform in [min_size, max_size] until `total`
+    plaintext bytes, random 24-byte nonces (every ~len/5-th about to carry out of byte 7,
+    cipher.go:665), each object's plaintext and wire body (crypt file minus its 32-byte
+    header, cipher.go:1121) 16-byte aligned in one plaintext image and one wire image.
+    Returns (sizes, nonces, pstart, wstart, plain_len, wire_len, desc, obj) with one seal
+    descriptor per 64 KiB block (plain -> wire; swap src/dst for open) and obj[i] = the
+    object of descriptor i."""
+    lo, hi = math.log(min_size), math.log(max_size)
+    sizes = []
+    acc = 0
+    while acc < total:
+        sz = int(math.exp(rng.uniform(lo, hi)))
+        sizes.append(sz)
+        acc += sz
+    nonces = [bytes(rng.integers(0, 256, 24, dtype=np.uint8)) for _ in sizes]
+    for o in range(0, len(sizes), max(1, len(sizes) // 5)):
+        nonces[o] = b"\xfe" + b"\xff" * 7 + nonces[o][8:]
+    pstart, wstart, p, w = [], [], 0, 0
+    nblk = [(sz + BLOCK_DATA - 1) // BLOCK_DATA for sz in sizes]
+    for sz, nb in zip(sizes, nblk):
+        pstart.append(p)
+        wstart.append(w)
+        p = _align16(p + sz)
+        w = _align16(w + sz + 16 * nb)
+    d = np.zeros(sum(nblk), dtype=DESC_DTYPE)
+    obj = np.zeros(len(d), dtype=np.int64)
+    k = 0
+    for o, sz in enumerate(sizes):
+        n = nblk[o]
+        i = np.arange(n, dtype=np.uint64)
+        sl = slice(k, k + n)
+        d["src"][sl] = pstart[o] + i * BLOCK_DATA
+        d["dst"][sl] = wstart[o] + i * BLOCK_SIZE
+        d["len"][sl] = np.minimum(BLOCK_DATA, sz - i.astype(np.int64) * BLOCK_DATA)
+        d["nonce"][sl] = nonce_plus(nonces[o], np.arange(n))
+        obj[sl] = o
+        k += n
+    return sizes, nonces, pstart, wstart, p, w, d, obj
 
 
 def reduce_counters(counters, dist=None, group=None):

@@ -12,14 +12,13 @@ object to return ErrorEncryptedBadBlock exactly at its first failing block
 
 RCLONE_AMD_CONFIG3_BYTES overrides the 10 GiB total (e.g. for a quick local run).
 """
-import math
 import os
 
 import numpy as np
 import pytest
 
 from oracle import pyoracle as orc
-from rclone_amd.shard import nonce_plus
+from rclone_amd.shard import mixed_object_layout
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -28,48 +27,11 @@ TOTAL = int(os.environ.get("RCLONE_AMD_CONFIG3_BYTES", 10 << 30))
 SEED = 0xC0F3
 BLOCK_DATA, BLOCK_SIZE = 65536, 65552
 MAGIC = b"RCLONE\x00\x00"
-DESC = np.dtype([("src", "<u8"), ("dst", "<u8"), ("len", "<u4"), ("res", "<u4"), ("nonce", "u1", (24,))])
-
-
-def _align16(x):
-    return (x + 15) & ~15
 
 
 def make_layout(total, rng):
     """Object sizes, nonces and the per-block descriptor table (plain <-> wire offsets)."""
-    lo, hi = math.log(4096), math.log(8 << 20)
-    sizes = []
-    acc = 0
-    while acc < total:
-        s = int(math.exp(rng.uniform(lo, hi)))
-        sizes.append(s)
-        acc += s
-    nonces = [bytes(rng.integers(0, 256, 24, dtype=np.uint8)) for _ in sizes]
-    # carry edges: nonce bytes 0..7 about to wrap (nonce.add carries into byte 8.., cipher.go:665)
-    for o in range(0, len(sizes), max(1, len(sizes) // 5)):
-        nonces[o] = b"\xfe" + b"\xff" * 7 + nonces[o][8:]
-    pstart, wstart, p, w = [], [], 0, 0
-    for s in sizes:
-        pstart.append(p)
-        wstart.append(w)
-        nb = (s + BLOCK_DATA - 1) // BLOCK_DATA
-        p = _align16(p + s)
-        w = _align16(w + s + 16 * nb)
-    nblk = [(s + BLOCK_DATA - 1) // BLOCK_DATA for s in sizes]
-    d = np.zeros(sum(nblk), dtype=DESC)
-    obj = np.zeros(len(d), dtype=np.int64)
-    k = 0
-    for o, s in enumerate(sizes):
-        n = nblk[o]
-        i = np.arange(n, dtype=np.uint64)
-        sl = slice(k, k + n)
-        d["src"][sl] = pstart[o] + i * BLOCK_DATA
-        d["dst"][sl] = wstart[o] + i * BLOCK_SIZE
-        d["len"][sl] = np.minimum(BLOCK_DATA, s - i.astype(np.int64) * BLOCK_DATA)
-        d["nonce"][sl] = nonce_plus(nonces[o], np.arange(n))
-        obj[sl] = o
-        k += n
-    return sizes, nonces, pstart, wstart, p, w, d, obj
+    return mixed_object_layout(total, rng)
 
 
 @pytest.fixture(scope="module")
