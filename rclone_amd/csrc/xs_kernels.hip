@@ -48,6 +48,9 @@
 #ifndef XS_DBUF  // double-buffered staging (8 KiB per wave)
 #define XS_DBUF 0
 #endif
+#ifndef XS_KEYGEN_WIDE_MAX  // batches up to this many blocks get one keygen wave per block (latency)
+#define XS_KEYGEN_WIDE_MAX 16
+#endif
 #ifndef XS_SPLIT_MAX  // batches up to this many blocks run four waves per block (latency)
 #define XS_SPLIT_MAX 256
 #endif
@@ -504,6 +507,9 @@ __device__ __forceinline__ void add5(P5& a, const P5& b) {
   for (int i = 0; i < 5; i++) a.v[i] += b.v[i];
 }
 
+__device__ void full_corr(bool seal, P5 sumA, P5 sumB, P5 sumC, P5 sumD4, const P5& r3, const P5& r32,
+                          const P5& r65, const P5& r66, const P5& W63, const uint32_t (&ks)[16], BlockKey* __restrict__ o);
+
 __device__ void full_tables(bool seal, const P5& r, const uint32_t (&ks)[16], BlockKey* __restrict__ o) {
   P5 one;
   one.v[0] = 1; one.v[1] = one.v[2] = one.v[3] = one.v[4] = 0;
@@ -544,6 +550,14 @@ __device__ void full_tables(bool seal, const P5& r, const uint32_t (&ks)[16], Bl
     add5(sumB, v);
   }
   const P5 W63 = pmul(w, v);
+  const P5 r65 = pmul(r64, r);
+  full_corr(seal, sumA, sumB, sumC, sumD4, r3, r32, r65, pmul(r65, r), W63, ks, o);
+}
+
+// corr from the table sums (sumA = sum A_i, sumB = sum B_j, sumC = sum C_b, sumD4 = D0+..+D3)
+// and r^3, r^32, r^65, r^66, r^4032 = W_63 (any pmul-bounded representatives).
+__device__ void full_corr(bool seal, P5 sumA, P5 sumB, P5 sumC, P5 sumD4, const P5& r3, const P5& r32,
+                          const P5& r65, const P5& r66, const P5& W63, const uint32_t (&ks)[16], BlockKey* __restrict__ o) {
   pnorm(sumA);
   pnorm(sumB);
   const P5 SW = pcanon(pmul(sumA, sumB));
@@ -552,7 +566,6 @@ __device__ void full_tables(bool seal, const P5& r, const uint32_t (&ks)[16], Bl
   P5 one_r32 = r32;
   one_r32.v[0] += 1;
   const P5 S = pcanon(pmul(pmul(pmul(r3, sumC), sumD4), one_r32));
-  const P5 r65 = pmul(r64, r), r66 = pmul(r65, r);
   P5 E, B, two128;
 #pragma unroll
   for (int i = 0; i < 5; i++) {
@@ -581,16 +594,11 @@ __device__ void full_tables(bool seal, const P5& r, const uint32_t (&ks)[16], Bl
 // One lane per crypt block.  MODE: 0 object seal, 1 object open, 2 descriptor seal,
 // 3 descriptor open.  Object mode derives nonce, offsets and length from the block
 // index (cipher.go:665-678 nonce.add; :1121 EncryptedSize layout).
+// Block b's nonce, offsets and length; false for a descriptor that fails validation.
 template <int MODE>
-__global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uint64_t first_block,
-                                                uint64_t total_len, uint64_t nblocks,
-                                                const xs_block_desc* __restrict__ desc,
-                                                BlockKey* __restrict__ out) {
-  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nblocks) return;
-  uint32_t n[6];
-  uint64_t src, dst;
-  uint32_t len;
+__device__ __forceinline__ bool block_params(const NonceArg& nonce0, uint64_t first_block, uint64_t total_len,
+                                             const xs_block_desc* __restrict__ desc, uint64_t b, uint32_t (&n)[6],
+                                             uint64_t& src, uint64_t& dst, uint32_t& len) {
   if constexpr (MODE < 2) {
     // 192-bit little-endian nonce0 + (first_block + b) == nonce.add (cipher.go:665)
     uint64_t add = first_block + b;
@@ -636,11 +644,25 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
     const uint64_t out_pay = dst + (MODE == 2 ? XS_BLOCK_HDR : 0u) + nonce0.n[5];
     const bool bad = len == 0 || len > XS_BLOCK_DATA || src > src_len || in_need > src_len - src ||
                      dst > dst_len || out_need > dst_len - dst || (in_pay & 15u) || (out_pay & 15u);
-    if (bad) {
-      out[b].flags = 1;
-      out[b].len = 0;
-      return;
-    }
+    if (bad) return false;
+  }
+  return true;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uint64_t first_block,
+                                                uint64_t total_len, uint64_t nblocks,
+                                                const xs_block_desc* __restrict__ desc,
+                                                BlockKey* __restrict__ out) {
+  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  uint32_t n[6];
+  uint64_t src, dst;
+  uint32_t len;
+  if (!block_params<MODE>(nonce0, first_block, total_len, desc, b, n, src, dst, len)) {
+    out[b].flags = 1;
+    out[b].len = 0;
+    return;
   }
   // HSalsa20(key, nonce[0:16]) -> subkey
   uint32_t x[16] = {SIG0, key.k[0], key.k[1], key.k[2], key.k[3], SIG1, n[0], n[1],
@@ -700,6 +722,156 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
   // r^253 = r^224 * r^29: the Horner gap between a lane's consecutive chunk groups
   // (64 lanes per block, 4 chunks per group: 4*64 - 3)
   put5(o->R, pmul(r224, r29));
+}
+
+// ---------------------------------------------------------------- keygen, one wave per block
+// For small batches (ranged reads, a decrypter's last blocks) the one-lane-per-block keygen is a
+// single lane's dependent chain (~50 field multiplies after three Salsa20 cores).  Here the 64
+// lanes of a wave share one block: lanes < 32 make keystream block 0 while lanes >= 32 make
+// block 1024 (one Salsa20 latency instead of two), and the table entries are built across
+// lanes (a wave issues one pmul for all lanes at once): full blocks in 13 pmul steps (levels
+// of base^0..base^8 for the bases r, r^8, r^64, r^512, three steps each, then W_63, r^65, r^66)
+// instead of the ~45 of full_tables' chains; partial blocks (lane 0..31 T1[i] = r^i, 32..39
+// T2[a] = r^(32a), 40 R = r^253) by square-and-multiply per lane, 8 steps.  The entries are
+// other representatives of the same residues (pmul-bounded, as the crypt kernels accept); corr
+// is canonical, so tags and ciphertext equal the narrow keygen's.
+template <int MODE>
+__global__ void __launch_bounds__(64) xs_keygen_wide(KeyArg key, NonceArg nonce0, uint64_t first_block,
+                                                     uint64_t total_len, uint64_t nblocks,
+                                                     const xs_block_desc* __restrict__ desc,
+                                                     BlockKey* __restrict__ out) {
+  const uint64_t b = blockIdx.x;
+  const uint32_t l = threadIdx.x;
+  if (b >= nblocks) return;  // uniform per workgroup
+  __shared__ uint32_t pw[64][5];
+  uint32_t n[6];
+  uint64_t src, dst;
+  uint32_t len;
+  BlockKey* o = out + b;
+  if (!block_params<MODE>(nonce0, first_block, total_len, desc, b, n, src, dst, len)) {
+    if (l == 0) {
+      o->flags = 1;
+      o->len = 0;
+    }
+    return;
+  }
+  uint32_t x[16] = {SIG0, key.k[0], key.k[1], key.k[2], key.k[3], SIG1, n[0], n[1],
+                    n[2], n[3],     SIG2,     key.k[4], key.k[5], key.k[6], key.k[7], SIG3};
+  salsa_rounds(x);
+  uint32_t sk[8] = {x[0], x[5], x[10], x[15], x[6], x[7], x[8], x[9]};
+  uint32_t ks[16];
+  salsa20_block(sk, n[4], n[5], l < 32 ? 0u : 1024u, ks);
+  if (l == 32 && len > XS_BLOCK_DATA - 32) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) o->ks1024[i] = ks[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) ks[i] = __shfl(ks[i], 0);  // block 0 words 0..7 (r, s) everywhere
+  P5 r;
+  r.v[0] = ks[0] & 0x3ffffffu;
+  r.v[1] = alignbit(ks[1], ks[0], 26) & 0x3ffff03u;
+  r.v[2] = alignbit(ks[2], ks[1], 20) & 0x3ffc0ffu;
+  r.v[3] = alignbit(ks[3], ks[2], 14) & 0x3f03fffu;
+  r.v[4] = (ks[3] >> 8) & 0x00fffffu;
+  if (l == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) o->subkey[i] = sk[i];
+    o->n2[0] = n[4];
+    o->n2[1] = n[5];
+    o->len = len;
+    o->flags = 0;
+    o->src = src;
+    o->dst = dst;
+#pragma unroll
+    for (int i = 0; i < 4; i++) o->s[i] = ks[4 + i];
+#pragma unroll
+    for (int i = 0; i < 5; i++) o->r[i] = r.v[i];
+  }
+  P5 p;
+  p.v[0] = 1; p.v[1] = 0; p.v[2] = 0; p.v[3] = 0; p.v[4] = 0;
+  if (len == XS_BLOCK_DATA) {
+    // Level m = 0..3 (bases r, r^8, r^64, r^512) lives in lanes 9m + b holding base^b,
+    // b = 0..8; three pmul steps per level (b = 2; 3, 4; 5..8), lane 9m + 8 = the next base.
+    if (l == 1) p = r;
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const uint32_t b = l - 9u * m;  // wraps for lanes below the level: not in 2..8
+#pragma unroll
+      for (int st = 0; st < 3; st++) {
+        // operands: st 0: b=2 <- 1*1; st 1: b=3 <- 2*1, b=4 <- 2*2; st 2: b=5..8 <- 4*(b-4)
+        const uint32_t lo = st == 0 ? 2u : st == 1 ? 3u : 5u, hi = st == 0 ? 2u : st == 1 ? 4u : 8u;
+        const bool act = b >= lo && b <= hi;
+        const uint32_t ia = 9u * m + (st == 0 ? 1u : st == 1 ? 2u : 4u);
+        const uint32_t ib = 9u * m + (act ? (st == 0 ? 1u : st == 1 ? b - 2u : b - 4u) : 0u);
+        P5 a, c;
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          a.v[i] = (uint32_t)__shfl((int)p.v[i], (int)ia);
+          c.v[i] = (uint32_t)__shfl((int)p.v[i], (int)ib);
+        }
+        const P5 q = pmul(a, c);
+        if (act) p = q;
+      }
+      if (m < 3) {  // next level: base^0 = 1, base^1 = this level's base^8
+        P5 nb;
+#pragma unroll
+        for (int i = 0; i < 5; i++) nb.v[i] = (uint32_t)__shfl((int)p.v[i], (int)(9u * m + 8u));
+        if (l == 9u * (m + 1) + 1u) p = nb;
+      }
+    }
+    // C[b] = lane b, D[a] = lane 9 + a, A[i] = lane 18 + i, B[j] = lane 27 + j;
+    // lane 36: W63 = A[7] B[7] = r^4032, lane 37: r^65 = A[1] C[1], lane 38: r^66 = A[1] C[2]
+    {
+      const uint32_t ia = l == 36u ? 25u : 19u, ib = l == 36u ? 34u : l == 37u ? 1u : 2u;
+      P5 a, c;
+#pragma unroll
+      for (int i = 0; i < 5; i++) {
+        a.v[i] = (uint32_t)__shfl((int)p.v[i], (int)ia);
+        c.v[i] = (uint32_t)__shfl((int)p.v[i], (int)ib);
+      }
+      const P5 q = pmul(a, c);
+      if (l >= 36u && l <= 38u) p = q;
+    }
+    if (l < 8) put5(o->full.C[l], p);
+    else if (l >= 9 && l < 18) put5(o->full.D[l - 9], p);
+    else if (l >= 18 && l < 26) put5(o->full.A[l - 18], p);
+    else if (l >= 27 && l < 35) put5(o->full.B[l - 27], p);
+#pragma unroll
+    for (int i = 0; i < 5; i++) pw[l][i] = p.v[i];
+    __syncthreads();
+    if (l == 0) {
+      P5 sumA, sumB, sumC, sumD4, v[5];
+#pragma unroll
+      for (int i = 0; i < 5; i++) {
+        sumC.v[i] = sumD4.v[i] = sumA.v[i] = sumB.v[i] = 0;
+        for (int k = 0; k < 8; k++) {
+          sumC.v[i] += pw[k][i];
+          sumA.v[i] += pw[18 + k][i];
+          sumB.v[i] += pw[27 + k][i];
+        }
+        for (int k = 0; k < 4; k++) sumD4.v[i] += pw[9 + k][i];
+        v[0].v[i] = pw[3][i];   // r^3
+        v[1].v[i] = pw[13][i];  // r^32 = D[4]
+        v[2].v[i] = pw[37][i];  // r^65
+        v[3].v[i] = pw[38][i];  // r^66
+        v[4].v[i] = pw[36][i];  // r^4032
+      }
+      full_corr(MODE == 0 || MODE == 2, sumA, sumB, sumC, sumD4, v[0], v[1], v[2], v[3], v[4], ks, o);
+    }
+    return;
+  }
+  // partial blocks (one per object at most): lane e's entry by square-and-multiply
+  const uint32_t e = l < 32 ? l : l < 40 ? 32u * (l - 32u) : l == 40 ? 253u : 0u;
+  P5 sq = r;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const P5 q = pmul(p, sq);
+    if ((e >> j) & 1u) p = q;
+    if (j < 7) sq = pmul(sq, sq);
+  }
+  if (l < 32) put5(o->part.T1[l], p);
+  else if (l < 40) put5(o->part.T2[l - 32], p);
+  else if (l == 40) put5(o->R, p);
 }
 
 // ---------------------------------------------------------------- main block kernel
@@ -1425,6 +1597,20 @@ hipError_t launch_keygen(int mode, const KeyArg& key, const NonceArg& nonce0, ui
                          uint64_t total_len, uint64_t nblocks, const xs_block_desc* desc, BlockKey* out,
                          hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
+  static const uint64_t wide_max = [] {  // env XS_KEYGEN_WIDE_MAX overrides (A/B, 0 = never)
+    const char* v = getenv("XS_KEYGEN_WIDE_MAX");
+    return v ? strtoull(v, nullptr, 10) : (uint64_t)XS_KEYGEN_WIDE_MAX;
+  }();
+  if (nblocks <= wide_max) {  // few blocks: one wave per block (latency)
+    const dim3 g((unsigned)nblocks);
+    switch (mode) {
+      case 0: hipLaunchKernelGGL(xs_keygen_wide<0>, g, dim3(64), 0, stream, key, nonce0, first_block, total_len, nblocks, desc, out); break;
+      case 1: hipLaunchKernelGGL(xs_keygen_wide<1>, g, dim3(64), 0, stream, key, nonce0, first_block, total_len, nblocks, desc, out); break;
+      case 2: hipLaunchKernelGGL(xs_keygen_wide<2>, g, dim3(64), 0, stream, key, nonce0, first_block, total_len, nblocks, desc, out); break;
+      default: hipLaunchKernelGGL(xs_keygen_wide<3>, g, dim3(64), 0, stream, key, nonce0, first_block, total_len, nblocks, desc, out); break;
+    }
+    return hipGetLastError();
+  }
   const uint64_t grid = (nblocks + 63) / 64;
   switch (mode) {
     case 0: hipLaunchKernelGGL(xs_keygen<0>, dim3((unsigned)grid), dim3(64), 0, stream, key, nonce0, first_block, total_len, nblocks, desc, out); break;

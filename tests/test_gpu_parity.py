@@ -175,3 +175,28 @@ def test_split_and_wave_paths_agree():
         o = out.cpu().numpy().tobytes()
         assert o[7 * 65536:8 * 65536] == bytes(65536)
         assert o[:7 * 65536] == plain[:7 * 65536] and o[8 * 65536:nb * 65536 - 65536] == plain[8 * 65536:nb * 65536 - 65536]
+
+
+def test_wide_and_narrow_keygen_agree(dev):
+    # batches of <= XS_KEYGEN_WIDE_MAX (16) blocks build their key schedules with one wave per
+    # block (xs_keygen_wide: table entries by square-and-multiply), larger ones with one lane per
+    # block (the multiply chains): the sealed bytes and verdicts must not depend on which.
+    # Tail lengths cover the partial-block tables, the ks1024 words (len > 65504) and a full block.
+    key = splitmix64_bytes(41, 32)
+    n0 = bytes([0xFD] + [0xFF] * 15 + list(splitmix64_bytes(42, 8)))  # nonce carries at block 3
+    big = 300
+    for tail in (1, 31, 32, 33, 4096, 65503, 65504, 65505, 65535, 65536):
+        plain = splitmix64_bytes(43 + tail, big * 65536 + tail)
+        whole = to_bytes(dev.seal_object(key, n0, to_dev(plain)))          # 301 blocks: narrow
+        part = dev.seal_object(key, n0, to_dev(plain[big * 65536:]), first_block=big)  # 1 block: wide
+        pb = to_bytes(part)
+        assert pb == whole[big * 65552:], tail
+        two = to_bytes(dev.seal_object(key, n0, to_dev(plain[(big - 1) * 65536:]), first_block=big - 1))
+        assert two == whole[(big - 1) * 65552:], tail
+        if tail in (33, 65505, 65536):
+            bad = to_dev(pb)
+            bad[16 + tail // 2] ^= 0x40
+            out, ok = dev.open_object(key, n0, bad, first_block=big)
+            assert to_bytes(ok)[:1] == b"\x00" and to_bytes(out) == bytes(tail), tail
+            out, ok = dev.open_object(key, n0, part, first_block=big)
+            assert to_bytes(out) == plain[big * 65536:] and to_bytes(ok)[:1] == b"\x01", tail
