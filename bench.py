@@ -464,7 +464,7 @@ def run_names(args, world, rank):
                        "kernel_names_per_s": round(n / (ke * 1e-3))},
             "cpu_baseline": None,
         }
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:  # the CPU baseline is an N=1 figure (rank 0 only)
             res["cpu_baseline"] = names_cpu_baseline(segs, c.name_key, c.name_tweak, 5.0)
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -642,7 +642,7 @@ def main():
                                                        int(counters[3].item()) & (2**64 - 1))},
             "cpu_baseline": None,
         }
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:  # the CPU baseline is an N=1 figure (rank 0 only)
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(res), flush=True)
     if world > 1:
