@@ -636,6 +636,17 @@ static int engine_issue_zero_copy(xs_engine::CSlot& c, const std::vector<uint64_
   const xs_block_desc* dd = (const xs_block_desc*)(uintptr_t)c.d_h_desc;
   uint64_t nseal = 0;
   hipError_t err = hipSuccess;
+  bool one_run = true;  // every request of the batch has the same direction and key
+  for (const auto* q : batch) one_run = one_run && q->seal == batch[0]->seal && !memcmp(q->key, batch[0]->key, 32);
+  if (one_run && nblk <= fused_max_blocks()) {  // tiny batch (a ranged read): one launch
+    const bool seal = batch[0]->seal;
+    err = launch_crypt_fused(seal, key_arg(batch[0]->key), bounds, dd, nblk, (const uint8_t*)(uintptr_t)sbase,
+                             (uint8_t*)(uintptr_t)dbase, seal ? nullptr : (uint8_t*)(uintptr_t)c.d_h_ok, st);
+    if (err != hipSuccess) return hip_fail(err, "zero-copy fused");
+    err = hipEventRecord(c.done, st);
+    if (err != hipSuccess) return hip_fail(err, "zero-copy event");
+    return XS_OK;
+  }
   for (size_t r = 0; r < batch.size();) {  // one keygen per run of (direction, key)
     size_t r1 = r + 1;
     while (r1 < batch.size() && batch[r1]->seal == batch[r]->seal && !memcmp(batch[r1]->key, batch[r]->key, 32)) r1++;

@@ -48,6 +48,9 @@
 #ifndef XS_DBUF  // double-buffered staging (8 KiB per wave)
 #define XS_DBUF 0
 #endif
+#ifndef XS_FUSED_MAX  // single-request descriptor batches up to this many blocks: keygen + crypt in one launch
+#define XS_FUSED_MAX 16
+#endif
 #ifndef XS_KEYGEN_WIDE_MAX  // batches up to this many blocks get one keygen wave per block (latency)
 #define XS_KEYGEN_WIDE_MAX 16
 #endif
@@ -735,19 +738,16 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
 // T2[a] = r^(32a), 40 R = r^253) by square-and-multiply per lane, 8 steps.  The entries are
 // other representatives of the same residues (pmul-bounded, as the crypt kernels accept); corr
 // is canonical, so tags and ciphertext equal the narrow keygen's.
+// The body: one wave (lanes l = threadIdx.x & 63) builds block b's key schedule into *o (global
+// memory, or LDS in the fused kernels); pw = 64 x 5 words of LDS scratch private to the wave.
 template <int MODE>
-__global__ void __launch_bounds__(64) xs_keygen_wide(KeyArg key, NonceArg nonce0, uint64_t first_block,
-                                                     uint64_t total_len, uint64_t nblocks,
-                                                     const xs_block_desc* __restrict__ desc,
-                                                     BlockKey* __restrict__ out) {
-  const uint64_t b = blockIdx.x;
-  const uint32_t l = threadIdx.x;
-  if (b >= nblocks) return;  // uniform per workgroup
-  __shared__ uint32_t pw[64][5];
+__device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& nonce0, uint64_t first_block,
+                                            uint64_t total_len, const xs_block_desc* __restrict__ desc,
+                                            uint64_t b, BlockKey* o, uint32_t (*pw)[5]) {
+  const uint32_t l = threadIdx.x & 63u;
   uint32_t n[6];
   uint64_t src, dst;
   uint32_t len;
-  BlockKey* o = out + b;
   if (!block_params<MODE>(nonce0, first_block, total_len, desc, b, n, src, dst, len)) {
     if (l == 0) {
       o->flags = 1;
@@ -838,7 +838,9 @@ __global__ void __launch_bounds__(64) xs_keygen_wide(KeyArg key, NonceArg nonce0
     else if (l >= 27 && l < 35) put5(o->full.B[l - 27], p);
 #pragma unroll
     for (int i = 0; i < 5; i++) pw[l][i] = p.v[i];
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (l == 0) {
       P5 sumA, sumB, sumC, sumD4, v[5];
 #pragma unroll
@@ -872,6 +874,16 @@ __global__ void __launch_bounds__(64) xs_keygen_wide(KeyArg key, NonceArg nonce0
   if (l < 32) put5(o->part.T1[l], p);
   else if (l < 40) put5(o->part.T2[l - 32], p);
   else if (l == 40) put5(o->R, p);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(64) xs_keygen_wide(KeyArg key, NonceArg nonce0, uint64_t first_block,
+                                                     uint64_t total_len, uint64_t nblocks,
+                                                     const xs_block_desc* __restrict__ desc,
+                                                     BlockKey* __restrict__ out) {
+  __shared__ uint32_t pw[64][5];
+  if (blockIdx.x >= nblocks) return;  // uniform per workgroup
+  keygen_wave<MODE>(key, nonce0, first_block, total_len, desc, blockIdx.x, out + blockIdx.x, pw);
 }
 
 // ---------------------------------------------------------------- main block kernel
@@ -1446,7 +1458,8 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
   return true;
 }
 
-template <bool SEAL, int NSPLIT>
+// FUSED: keys is the workgroup's own key schedule (LDS, built by keygen_wave), blk = workgroup.
+template <bool SEAL, int NSPLIT, bool FUSED = false>
 __device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, uint64_t nblocks,
                                            const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                            uint8_t* __restrict__ ok, uint32_t* lds) {
@@ -1460,9 +1473,10 @@ __device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, ui
 #else
   const uint32_t wg = blockIdx.x;
 #endif
-  const uint64_t blk = NSPLIT == 1 ? (uint64_t)wg * 4u + (uint64_t)__builtin_amdgcn_readfirstlane(wave) : (uint64_t)wg;
+  const uint64_t blk = FUSED ? (uint64_t)blockIdx.x
+                     : NSPLIT == 1 ? (uint64_t)wg * 4u + (uint64_t)__builtin_amdgcn_readfirstlane(wave) : (uint64_t)wg;
   if (blk >= nblocks) return;
-  const BlockKey* bk = keys + blk;
+  const BlockKey* bk = FUSED ? keys : keys + blk;
   if (bk->flags) {  // rejected descriptor: write nothing
     if (!SEAL && l == 0 && (NSPLIT == 1 || wave == 0u)) ok[blk] = 0;
     return;
@@ -1562,6 +1576,22 @@ xs_open(const BlockKey* __restrict__ keys, uint64_t nblocks, const uint8_t* __re
 #if XS_POLY_MFMA
 // Small batches (latency: a lone ranged read, a few coalesced handles): one block per
 // workgroup, four waves on four super-iterations each.
+// Tiny descriptor batches (ranged reads): keygen and the split crypt kernel in one launch.  Wave 0
+// builds the block's key schedule in LDS (keygen_wave), then the four waves seal / open it as
+// xs_seal_split / xs_open_split do.  Saves the second launch and the key schedule's HBM round trip.
+template <bool SEAL>
+__global__ void __launch_bounds__(256) xs_crypt_fused(KeyArg key, NonceArg bounds, const xs_block_desc* __restrict__ desc,
+                                                      uint64_t nblocks, const uint8_t* __restrict__ src,
+                                                      uint8_t* __restrict__ dst, uint8_t* __restrict__ ok) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
+  __shared__ BlockKey kl;
+  __shared__ uint32_t pw[64][5];
+  if (blockIdx.x >= nblocks) return;  // uniform per workgroup
+  if (threadIdx.x < 64) keygen_wave<SEAL ? 2 : 3>(key, bounds, 0, 0, desc, blockIdx.x, &kl, pw);
+  __syncthreads();
+  crypt_wave<SEAL, 4, true>(&kl, nblocks, src, dst, ok, lds);
+}
+
 __global__ void __launch_bounds__(256) xs_seal_split(const BlockKey* __restrict__ keys, uint64_t nblocks,
                                                      const uint8_t* __restrict__ src, uint8_t* __restrict__ dst) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
@@ -1645,6 +1675,26 @@ hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const
   if (seal) hipLaunchKernelGGL(xs_seal, dim3(grid), dim3(256), 0, stream, keys, nblocks, src, dst);
   else hipLaunchKernelGGL(xs_open, dim3(grid), dim3(256), 0, stream, keys, nblocks, src, dst, ok);
   return hipGetLastError();
+}
+
+hipError_t launch_crypt_fused(bool seal, const KeyArg& key, const NonceArg& bounds, const xs_block_desc* desc,
+                              uint64_t nblocks, const uint8_t* src, uint8_t* dst, uint8_t* ok, hipStream_t stream) {
+  if (nblocks == 0) return hipSuccess;
+  if (seal) hipLaunchKernelGGL(xs_crypt_fused<true>, dim3((unsigned)nblocks), dim3(256), 0, stream, key, bounds, desc, nblocks, src, dst, ok);
+  else hipLaunchKernelGGL(xs_crypt_fused<false>, dim3((unsigned)nblocks), dim3(256), 0, stream, key, bounds, desc, nblocks, src, dst, ok);
+  return hipGetLastError();
+}
+
+uint64_t fused_max_blocks() {
+#if XS_POLY_MFMA
+  static const uint64_t m = [] {  // env XS_FUSED_MAX overrides (A/B, 0 = never)
+    const char* v = getenv("XS_FUSED_MAX");
+    return v ? strtoull(v, nullptr, 10) : (uint64_t)XS_FUSED_MAX;
+  }();
+  return m;
+#else
+  return 0;  // the split kernels need the matrix-core Poly1305
+#endif
 }
 
 hipError_t launch_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t first_block, uint64_t stride,
