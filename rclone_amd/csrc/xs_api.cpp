@@ -303,6 +303,11 @@ struct xs_engine {
     xs_block_desc* h_desc = nullptr;  // pinned
     uint8_t* h_ok = nullptr;          // pinned: verdicts of a zero-copy batch
     uint64_t d_h_desc = 0, d_h_ok = 0;  // their device addresses
+    uint32_t* h_flag = nullptr;  // pinned completion word of a fused batch (the kernel stores seq)
+    uint64_t d_h_flag = 0;
+    uint32_t* d_ctr = nullptr;   // workgroups finished (the last one resets it and stores the word)
+    uint32_t seq = 0;
+    bool spin = false;           // wait by polling h_flag instead of the event
     bool zc = false;
     std::vector<Req*> batch;
     uint64_t blocks = 0;
@@ -378,6 +383,8 @@ static void engine_free(xs_engine* e) {
     (void)hipFree(c.keys);
     (void)hipHostFree(c.h_desc);
     (void)hipHostFree(c.h_ok);
+    (void)hipHostFree(c.h_flag);
+    (void)hipFree(c.d_ctr);
     if (c.done) (void)hipEventDestroy(c.done);
     if (c.s) (void)hipStreamDestroy(c.s);
   }
@@ -431,7 +438,10 @@ extern "C" xs_engine* xs_engine_create(int device, uint32_t batch_blocks, int ns
         hipMalloc(&c.keys, (size_t)batch_blocks * sizeof(BlockKey)) != hipSuccess ||
         hipHostMalloc(&c.h_desc, (size_t)batch_blocks * sizeof(xs_block_desc), hipHostMallocPortable) != hipSuccess ||
         hipHostMalloc(&c.h_ok, batch_blocks, hipHostMallocPortable) != hipSuccess ||
-        !host_dev_ptr(c.h_desc, &c.d_h_desc, device) || !host_dev_ptr(c.h_ok, &c.d_h_ok, device)) {
+        !host_dev_ptr(c.h_desc, &c.d_h_desc, device) || !host_dev_ptr(c.h_ok, &c.d_h_ok, device) ||
+        hipHostMalloc(&c.h_flag, 64, hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        !host_dev_ptr(c.h_flag, &c.d_h_flag, device) || hipMalloc(&c.d_ctr, 4) != hipSuccess ||
+        hipMemset(c.d_ctr, 0, 4) != hipSuccess) {
       set_error("xs_engine_create: device allocation failed");
       engine_free(e);
       return nullptr;
@@ -616,6 +626,15 @@ static void nonce_plus(uint8_t out[24], const uint8_t n0[24], uint64_t x) {
 
 static NonceArg bounds_arg(uint64_t src_len, uint64_t dst_len);
 
+// Wait for fused batches by polling their completion word (XS_ENGINE_SPIN=0: the event only).
+static bool spin_wait() {
+  static const bool on = [] {
+    const char* v = getenv("XS_ENGINE_SPIN");
+    return v ? atoi(v) != 0 : true;
+  }();
+  return on;
+}
+
 // Zero-copy form of a combined batch (descriptors already in the pinned h_desc, offsets from
 // the lowest caller input / output address): keygen reads the descriptors from host memory,
 // the crypt kernels read the callers' inputs and write their outputs over PCIe, verdicts land
@@ -638,10 +657,14 @@ static int engine_issue_zero_copy(xs_engine::CSlot& c, const std::vector<uint64_
   hipError_t err = hipSuccess;
   bool one_run = true;  // every request of the batch has the same direction and key
   for (const auto* q : batch) one_run = one_run && q->seal == batch[0]->seal && !memcmp(q->key, batch[0]->key, 32);
+  c.spin = false;
   if (one_run && nblk <= fused_max_blocks()) {  // tiny batch (a ranged read): one launch
     const bool seal = batch[0]->seal;
+    c.seq++;
     err = launch_crypt_fused(seal, key_arg(batch[0]->key), bounds, dd, nblk, (const uint8_t*)(uintptr_t)sbase,
-                             (uint8_t*)(uintptr_t)dbase, seal ? nullptr : (uint8_t*)(uintptr_t)c.d_h_ok, st);
+                             (uint8_t*)(uintptr_t)dbase, seal ? nullptr : (uint8_t*)(uintptr_t)c.d_h_ok,
+                             spin_wait() ? c.d_ctr : nullptr, (uint32_t*)(uintptr_t)c.d_h_flag, c.seq, st);
+    c.spin = spin_wait();
     if (err != hipSuccess) return hip_fail(err, "zero-copy fused");
     err = hipEventRecord(c.done, st);
     if (err != hipSuccess) return hip_fail(err, "zero-copy event");
@@ -674,6 +697,7 @@ static int engine_issue_zero_copy(xs_engine::CSlot& c, const std::vector<uint64_
 // Issue one combined batch on coalescing slot c (asynchronously; completion = c.done).
 static int engine_issue_batch(xs_engine* e, xs_engine::CSlot& c) {
   auto& batch = c.batch;
+  c.spin = false;  // only a fused zero-copy launch sets it
   if (hipSetDevice(e->device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
   // seal requests first, then open; inside a direction, requests with equal keys adjacent
   std::stable_sort(batch.begin(), batch.end(), [](const xs_engine::Req* a, const xs_engine::Req* b) {
@@ -807,7 +831,19 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
       auto& c = e->cslots[head];
       lk.unlock();
       if (c.rc == XS_OK) {
-        hipError_t err = hipEventSynchronize(c.done);
+        // a fused batch stores its completion word (after its outputs, system scope): poll it,
+        // falling back to the event if the stream ends (or fails) without it
+        bool seen = false;
+        if (c.spin) {
+          for (unsigned k = 1;; k++) {
+            if (__atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) == c.seq) {
+              seen = true;
+              break;
+            }
+            if ((k & 1023u) == 0 && hipEventQuery(c.done) != hipErrorNotReady) break;
+          }
+        }
+        hipError_t err = seen ? hipSuccess : hipEventSynchronize(c.done);
         if (err != hipSuccess) c.rc = hip_fail(err, "coalesced stream");
       } else {
         (void)hipStreamSynchronize(c.s);

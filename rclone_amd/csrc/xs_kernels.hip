@@ -1582,14 +1582,28 @@ xs_open(const BlockKey* __restrict__ keys, uint64_t nblocks, const uint8_t* __re
 template <bool SEAL>
 __global__ void __launch_bounds__(256) xs_crypt_fused(KeyArg key, NonceArg bounds, const xs_block_desc* __restrict__ desc,
                                                       uint64_t nblocks, const uint8_t* __restrict__ src,
-                                                      uint8_t* __restrict__ dst, uint8_t* __restrict__ ok) {
+                                                      uint8_t* __restrict__ dst, uint8_t* __restrict__ ok,
+                                                      uint32_t* __restrict__ ctr, uint32_t* __restrict__ flag,
+                                                      uint32_t seq) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
   __shared__ BlockKey kl;
   __shared__ uint32_t pw[64][5];
-  if (blockIdx.x >= nblocks) return;  // uniform per workgroup
+  if (blockIdx.x >= nblocks) return;  // uniform per workgroup (grid == nblocks)
   if (threadIdx.x < 64) keygen_wave<SEAL ? 2 : 3>(key, bounds, 0, 0, desc, blockIdx.x, &kl, pw);
   __syncthreads();
   crypt_wave<SEAL, 4, true>(&kl, nblocks, src, dst, ok, lds);
+  if (ctr) {  // completion word: every wave's outputs at system scope, then the last workgroup signals
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == (uint32_t)nblocks - 1u) {
+        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence_system();
+        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
 }
 
 __global__ void __launch_bounds__(256) xs_seal_split(const BlockKey* __restrict__ keys, uint64_t nblocks,
@@ -1678,10 +1692,11 @@ hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const
 }
 
 hipError_t launch_crypt_fused(bool seal, const KeyArg& key, const NonceArg& bounds, const xs_block_desc* desc,
-                              uint64_t nblocks, const uint8_t* src, uint8_t* dst, uint8_t* ok, hipStream_t stream) {
+                              uint64_t nblocks, const uint8_t* src, uint8_t* dst, uint8_t* ok, uint32_t* ctr,
+                              uint32_t* flag, uint32_t seq, hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
-  if (seal) hipLaunchKernelGGL(xs_crypt_fused<true>, dim3((unsigned)nblocks), dim3(256), 0, stream, key, bounds, desc, nblocks, src, dst, ok);
-  else hipLaunchKernelGGL(xs_crypt_fused<false>, dim3((unsigned)nblocks), dim3(256), 0, stream, key, bounds, desc, nblocks, src, dst, ok);
+  if (seal) hipLaunchKernelGGL(xs_crypt_fused<true>, dim3((unsigned)nblocks), dim3(256), 0, stream, key, bounds, desc, nblocks, src, dst, ok, ctr, flag, seq);
+  else hipLaunchKernelGGL(xs_crypt_fused<false>, dim3((unsigned)nblocks), dim3(256), 0, stream, key, bounds, desc, nblocks, src, dst, ok, ctr, flag, seq);
   return hipGetLastError();
 }
 
