@@ -160,6 +160,32 @@ uint64_t xs_put_body_bytes(uint64_t nobj, const uint64_t *lens);
 void xs_engine_set_coalesce(xs_engine *e, int on);
 /* Cumulative coalescing counters: out[0] combined batches, out[1] requests, out[2] blocks. */
 void xs_engine_stats(xs_engine *e, uint64_t out[3]);
+/* Objects routed off the GPU MD5 lanes by xs_engine_seal_md5 / xs_engine_put_batch: the
+ * longest objects of a group are hashed on host cores over the GPU-sealed wire body when that
+ * shortens the group (one GPU lane does ~70 MB/s, one core ~10x that).  threads = host MD5
+ * workers (0 = every object on the GPU; default XS_MD5_HOST_THREADS or half the cores, <= 8).
+ * out[0] = objects hashed on the host so far, out[1] = their wire bytes. */
+void xs_engine_set_host_md5(xs_engine *e, int threads);
+void xs_engine_md5_stats(xs_engine *e, uint64_t out[2]);
+
+/* Multi-device engine pool: one process spreads its objects over several GPUs (or several
+ * engines per GPU).  devices = HIP device ids, repeats allowed ("0,0,0,0" = four engines on
+ * device 0); NULL / ndevices <= 0 -> env RCLONE_AMD_DEVICES (comma list), else RCLONE_AMD_DEVICE,
+ * else every visible device.  xs_pool_next hands out engines round-robin (one per object
+ * stream, fs/sync/sync.go:544 --transfers); xs_pool_seal_md5 / xs_pool_put_batch split their
+ * objects into contiguous byte-balanced ranges run concurrently, one engine each, with results
+ * identical to one engine's. */
+typedef struct xs_pool xs_pool;
+xs_pool *xs_pool_create(const int *devices, int ndevices, uint32_t batch_blocks, int nslots);
+void xs_pool_destroy(xs_pool *p);
+int xs_pool_size(const xs_pool *p);
+xs_engine *xs_pool_engine(xs_pool *p, int i);
+xs_engine *xs_pool_next(xs_pool *p);
+int xs_pool_seal_md5(xs_pool *p, const uint8_t key[32], uint64_t nobj, const uint8_t *nonces,
+                     const uint64_t *offs, const uint64_t *lens, const void *plain, uint8_t *md5);
+int xs_pool_put_batch(xs_pool *p, const uint8_t key[32], uint64_t nobj, const uint8_t *nonces,
+                      const uint64_t *offs, const uint64_t *lens, const void *plain, void *body, uint8_t *md5);
+
 /* Pinned (page-locked) host memory. */
 void *xs_host_alloc(size_t bytes);
 void xs_host_free(void *p);
@@ -214,8 +240,15 @@ int32_t rc_cipher_key(rc_cipher *c, const char *password, const char *salt);
 void rc_cipher_keys(const rc_cipher *c, uint8_t data_key[32], uint8_t name_key[32], uint8_t name_tweak[16]);
 void rc_cipher_set_pass_bad_blocks(rc_cipher *c, int32_t pass); /* setPassBadBlocks :217 */
 void rc_cipher_set_rand(rc_cipher *c, rc_reader rand);           /* c.cryptoRand */
-/* Blocks staged per GPU submission by encrypters/decrypters (default 64 = 4 MiB). */
+/* Read-ahead of encrypters/decrypters.  The first refill of a stream, and the first after a
+ * seek, reads first_blocks blocks (default 1: exactly what encrypter.Read / fillBuffer read,
+ * cipher.go:726-741, :862-898); each later refill doubles, up to batch_blocks per GPU submission
+ * (default 64 = 4 MiB).  first_blocks = 0: every refill reads batch_blocks. */
 void rc_cipher_set_batch_blocks(rc_cipher *c, uint32_t blocks);
+void rc_cipher_set_readahead(rc_cipher *c, uint32_t first_blocks);
+/* GPU engines used by this cipher's handles and batches (NULL: the process-wide pool over
+ * RCLONE_AMD_DEVICES / RCLONE_AMD_DEVICE / every device).  The pool must outlive the cipher. */
+void rc_cipher_set_pool(rc_cipher *c, xs_pool *pool);
 void rc_cipher_free(rc_cipher *c);
 
 int64_t rc_encrypted_size(int64_t size);               /* EncryptedSize :1121 */

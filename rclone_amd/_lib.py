@@ -66,6 +66,15 @@ _SIGS = [
     ("xs_put_body_bytes", u64, [u64, vp]),
     ("xs_engine_set_coalesce", None, [vp, ctypes.c_int]),
     ("xs_engine_stats", None, [vp, vp]),
+    ("xs_engine_set_host_md5", None, [vp, ctypes.c_int]),
+    ("xs_engine_md5_stats", None, [vp, vp]),
+    ("xs_pool_create", vp, [vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_int]),
+    ("xs_pool_destroy", None, [vp]),
+    ("xs_pool_size", ctypes.c_int, [vp]),
+    ("xs_pool_engine", vp, [vp, ctypes.c_int]),
+    ("xs_pool_next", vp, [vp]),
+    ("xs_pool_seal_md5", ctypes.c_int, [vp, ctypes.c_char_p, u64, vp, vp, vp, vp, vp]),
+    ("xs_pool_put_batch", ctypes.c_int, [vp, ctypes.c_char_p, u64, vp, vp, vp, vp, vp, vp]),
     ("xs_host_alloc", vp, [ctypes.c_size_t]),
     ("xs_host_free", None, [vp]),
     # cipher.go mirror
@@ -75,6 +84,8 @@ _SIGS = [
     ("rc_cipher_set_pass_bad_blocks", None, [vp, i32]),
     ("rc_cipher_set_rand", None, [vp, RcReader]),
     ("rc_cipher_set_batch_blocks", None, [vp, ctypes.c_uint32]),
+    ("rc_cipher_set_readahead", None, [vp, ctypes.c_uint32]),
+    ("rc_cipher_set_pool", None, [vp, vp]),
     ("rc_cipher_free", None, [vp]),
     ("rc_encrypted_size", i64, [i64]),
     ("rc_decrypted_size", i64, [i64, ctypes.POINTER(i32)]),

@@ -21,6 +21,7 @@
 
 #include <cerrno>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -61,22 +62,27 @@ int64_t read_fill(const rc_reader& r, uint8_t* buf, int64_t len, int32_t* err) {
   return n;
 }
 
-// ---------------------------------------------------------------- GPU engine (process-wide)
-std::mutex g_engine_mu;
-xs_engine* g_engine = nullptr;
-bool g_engine_failed = false;
+// ---------------------------------------------------------------- GPU engines (process-wide)
+// One pool of engines for the process, over every device in RCLONE_AMD_DEVICES (or
+// RCLONE_AMD_DEVICE, or all visible devices): each encrypter / decrypter takes an engine
+// round-robin when it first needs the GPU, so the transfers of one rclone process spread over the
+// node's GPUs (fs/sync/sync.go:544 startTransfers); a cipher may be bound to its own pool
+// (rc_cipher_set_pool).
+std::mutex g_pool_create_mu;
+xs_pool* g_xs_pool = nullptr;
+bool g_xs_pool_failed = false;
 
-xs_engine* engine() {
-  std::lock_guard<std::mutex> g(g_engine_mu);
-  if (g_engine || g_engine_failed) return g_engine;
-  int dev = 0;
-  if (const char* s = getenv("RCLONE_AMD_DEVICE")) dev = atoi(s);
+xs_pool* process_pool() {
+  std::lock_guard<std::mutex> g(g_pool_create_mu);
+  if (g_xs_pool || g_xs_pool_failed) return g_xs_pool;
   uint32_t batch = 256;
   if (const char* s = getenv("RCLONE_AMD_ENGINE_BLOCKS")) batch = (uint32_t)atoi(s);
-  g_engine = xs_engine_create(dev, batch, 3);
-  if (!g_engine) g_engine_failed = true;
-  return g_engine;
+  g_xs_pool = xs_pool_create(nullptr, 0, batch, 3);
+  if (!g_xs_pool) g_xs_pool_failed = true;
+  return g_xs_pool;
 }
+
+xs_pool* cipher_pool(const rc_cipher* c) { return c->pool ? c->pool : process_pool(); }
 
 // Pinned staging pool -- the counterpart of the reference's Cipher.buffers sync.Pool
 // (cipher.go:179, :255-262): handles come and go per object, and hipHostMalloc/hipHostFree
@@ -84,7 +90,9 @@ xs_engine* engine() {
 // keeping at most kPoolBytes cached.
 constexpr size_t kPoolBytes = (size_t)1 << 30;
 std::mutex g_pool_mu;
-std::multimap<size_t, uint8_t*> g_pool;
+// process-lifetime cache, deliberately never destroyed: buffers stay reachable (no exit-time
+// hipHostFree after the HIP runtime may already be torn down)
+std::multimap<size_t, uint8_t*>& g_pool = *new std::multimap<size_t, uint8_t*>();
 size_t g_pool_cached = 0;
 
 uint8_t* pool_get(size_t bytes, size_t* cap) {
@@ -191,6 +199,8 @@ extern "C" void rc_cipher_keys(const rc_cipher* c, uint8_t data_key[32], uint8_t
 extern "C" void rc_cipher_set_pass_bad_blocks(rc_cipher* c, int32_t pass) { c->pass_bad_blocks = pass != 0; }
 extern "C" void rc_cipher_set_rand(rc_cipher* c, rc_reader rand) { c->rand = rand; }
 extern "C" void rc_cipher_set_batch_blocks(rc_cipher* c, uint32_t blocks) { c->batch_blocks = blocks ? blocks : 1; }
+extern "C" void rc_cipher_set_readahead(rc_cipher* c, uint32_t first_blocks) { c->first_blocks = first_blocks; }
+extern "C" void rc_cipher_set_pool(rc_cipher* c, xs_pool* pool) { c->pool = pool; }
 extern "C" void rc_cipher_free(rc_cipher* c) { delete c; }
 
 // ---------------------------------------------------------------- sizes, nonce arithmetic
@@ -300,12 +310,28 @@ extern "C" const char* rc_error_string(int32_t e) {
 }
 
 // ---------------------------------------------------------------- encrypter
+// Read-ahead: the first refill of a stream (and the first after a seek) reads exactly one block,
+// as encrypter.Read / fillBuffer do (cipher.go:726-741, :862-898); each later refill doubles, up
+// to the cipher's batch_blocks, so a slow or streaming source sees the reference's first-byte
+// behaviour and a long one reaches full GPU batches after a few refills.
+static uint32_t next_batch(const rc_cipher* c, uint32_t* grow) {
+  const uint32_t cap = c->batch_blocks;
+  if (*grow == 0) *grow = c->first_blocks ? c->first_blocks : cap;  // 0: full batches at once
+  const uint32_t n = std::min(*grow, cap);
+  *grow = (uint32_t)std::min<uint64_t>((uint64_t)*grow * 2, cap);
+  return n;
+}
+
 struct rc_encrypter {
   std::mutex mu;
   rc_reader in{};
   rc_cipher* c = nullptr;
+  xs_engine* eng = nullptr;  // taken from the cipher's pool at the first refill
   uint8_t nonce[24] = {0};  // fh.nonce: initial nonce + blocks sealed
-  PinnedBuf plain, wire;    // staging (fh.readBuf / fh.buf)
+  uint8_t hdr[kFileHdr];    // magic || initial nonce, served before the first block
+  bool in_hdr = true;
+  PinnedBuf plain, wire;    // staging (fh.readBuf / fh.buf), allocated at the first refill
+  uint32_t grow = 0;        // read-ahead blocks of the next refill (next_batch)
   int64_t buf_index = 0, buf_size = 0;
   int32_t err = RC_NIL;
   bool finished = false;
@@ -353,14 +379,8 @@ extern "C" rc_encrypter* rc_encrypt_data(rc_cipher* c, rc_reader in, const uint8
       return nullptr;
     }
   }
-  const uint32_t batch = c->batch_blocks;
-  if (!fh->plain.ensure((size_t)batch * kBlockData) || !fh->wire.ensure((size_t)batch * kBlockSize + kFileHdr)) {
-    if (err) *err = RC_ERR_GPU;
-    delete fh;
-    return nullptr;
-  }
-  memcpy(fh->wire.p, kMagic, 8);
-  memcpy(fh->wire.p + 8, fh->nonce, 24);
+  memcpy(fh->hdr, kMagic, 8);
+  memcpy(fh->hdr + 8, fh->nonce, 24);
   fh->buf_size = kFileHdr;
   return fh;
 }
@@ -373,8 +393,12 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
     return 0;
   }
   if (fh->buf_index >= fh->buf_size) {
-    // refill: ReadFill block by block exactly as encrypter.Read would, up to batch blocks
-    const uint32_t batch = fh->c->batch_blocks;
+    // refill: ReadFill block by block exactly as encrypter.Read would, up to next_batch blocks
+    fh->in_hdr = false;
+    const uint32_t batch = next_batch(fh->c, &fh->grow);
+    if (!fh->plain.ensure((size_t)fh->c->batch_blocks * kBlockData) ||
+        !fh->wire.ensure((size_t)fh->c->batch_blocks * kBlockSize))
+      return enc_finish(fh, RC_ERR_GPU, err);
     int64_t total = 0;
     uint32_t nb = 0;
     int32_t first_err = RC_NIL;
@@ -392,8 +416,9 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
       }
     }
     if (nb == 0) return enc_finish(fh, first_err, err);
-    xs_engine* eng = engine();
-    if (!eng || xs_engine_seal(eng, fh->c->data_key, fh->nonce, 0, fh->plain.p, (uint64_t)total, fh->wire.p) != XS_OK)
+    if (!fh->eng) fh->eng = xs_pool_next(cipher_pool(fh->c));
+    if (!fh->eng ||
+        xs_engine_seal(fh->eng, fh->c->data_key, fh->nonce, 0, fh->plain.p, (uint64_t)total, fh->wire.p) != XS_OK)
       return enc_finish(fh, RC_ERR_GPU, err);
     fh->buf_index = 0;
     fh->buf_size = total + (int64_t)nb * kBlockHdr;
@@ -401,7 +426,7 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
   }
   int64_t m = fh->buf_size - fh->buf_index;
   if (m > n) m = n;
-  memcpy(p, fh->wire.p + fh->buf_index, (size_t)m);
+  memcpy(p, (fh->in_hdr ? fh->hdr : fh->wire.p) + fh->buf_index, (size_t)m);
   fh->buf_index += m;
   return m;
 }
@@ -417,6 +442,8 @@ struct rc_decrypter {
   uint8_t nonce[24] = {0};
   uint8_t initial_nonce[24] = {0};
   rc_cipher* c = nullptr;
+  xs_engine* eng = nullptr;  // taken from the cipher's pool at the first refill
+  uint32_t grow = 0;         // read-ahead blocks of the next refill (next_batch); 0 after open/seek
   PinnedBuf wire, plain, okb;
   // decoded batch: blocks [cur, nblk) still to serve; block i has payload length blen[i]
   std::vector<int64_t> blen;
@@ -434,6 +461,8 @@ struct rc_decrypter {
   int32_t wrapped = RC_NIL;
 };
 
+// staging for a full batch, allocated when the first block is read (not at open: a header
+// error or a failing source never needs it)
 static bool dec_alloc(rc_decrypter* fh) {
   const uint32_t batch = fh->c->batch_blocks;
   return fh->wire.ensure((size_t)batch * kBlockSize) && fh->plain.ensure((size_t)batch * kBlockData) &&
@@ -454,13 +483,12 @@ static int32_t dec_finish(rc_decrypter* fh, int32_t err) {
 }
 
 // unFinish (cipher.go:1054-1066)
-static bool dec_unfinish(rc_decrypter* fh) {
+static void dec_unfinish(rc_decrypter* fh) {
   fh->finished = false;
   fh->err = RC_NIL;
   fh->buf_index = fh->buf_size = 0;
   fh->nblk = fh->cur = 0;
   fh->have_tail = false;
-  return dec_alloc(fh);
 }
 
 static int32_t dec_close_locked(rc_decrypter* fh) {
@@ -475,8 +503,9 @@ static int32_t dec_close_locked(rc_decrypter* fh) {
 // the GPU.  Errors are not returned here; they are queued at the block position where
 // fillBuffer (cipher.go:862-898) would return them.
 static int32_t dec_read_batch(rc_decrypter* fh, uint32_t want) {
-  const uint32_t batch = fh->c->batch_blocks;
-  if (want == 0 || want > batch) want = batch;
+  const uint32_t ra = next_batch(fh->c, &fh->grow);
+  if (want == 0 || want > ra) want = ra;
+  if (!dec_alloc(fh)) return RC_ERR_GPU;
   fh->blen.assign(want, 0);
   fh->berr.assign(want, RC_NIL);
   fh->nblk = fh->cur = 0;
@@ -506,9 +535,9 @@ static int32_t dec_read_batch(rc_decrypter* fh, uint32_t want) {
   }
   fh->nblk = nb;
   if (nb == 0) return RC_NIL;
-  xs_engine* eng = engine();
-  if (!eng || xs_engine_open(eng, fh->c->data_key, fh->nonce, 0, fh->wire.p, (uint64_t)total, fh->plain.p,
-                             fh->okb.p) != XS_OK) {
+  if (!fh->eng) fh->eng = xs_pool_next(cipher_pool(fh->c));
+  if (!fh->eng || xs_engine_open(fh->eng, fh->c->data_key, fh->nonce, 0, fh->wire.p, (uint64_t)total, fh->plain.p,
+                                 fh->okb.p) != XS_OK) {
     fh->nblk = 0;
     return RC_ERR_GPU;
   }
@@ -551,12 +580,6 @@ static rc_decrypter* new_decrypter(rc_cipher* c, rc_reader rc, int32_t* err) {
   fh->rc = rc;
   fh->have_rc = true;
   fh->c = c;
-  if (!dec_alloc(fh)) {
-    *err = RC_ERR_GPU;
-    dec_close_locked(fh);
-    delete fh;
-    return nullptr;
-  }
   uint8_t hdr[kFileHdr];
   int32_t e = RC_NIL;
   int64_t n = read_fill(fh->rc, hdr, kFileHdr, &e);
@@ -678,10 +701,7 @@ static int64_t range_seek_locked(rc_decrypter* fh, int64_t offset, int32_t whenc
     return 0;
   }
   if (fh->finished && fh->err == RC_EOF) {
-    if (!dec_unfinish(fh)) {
-      *err = dec_finish(fh, RC_ERR_GPU);
-      return 0;
-    }
+    dec_unfinish(fh);
   } else if (fh->finished) {
     *err = fh->err;
     return 0;
@@ -691,10 +711,11 @@ static int64_t range_seek_locked(rc_decrypter* fh, int64_t offset, int32_t whenc
   const int64_t uoff = u[0], ulim = u[1], discard = u[2], blocks = u[3];
   memcpy(fh->nonce, fh->initial_nonce, 24);
   rc_nonce_add(fh->nonce, (uint64_t)blocks);
-  // drop read-ahead
+  // drop read-ahead; the first refill after the seek reads one block again
   fh->nblk = fh->cur = 0;
   fh->have_tail = false;
   fh->buf_index = fh->buf_size = 0;
+  fh->grow = 0;
   if (fh->have_rc && fh->rc.range_seek) {
     int32_t e = fh->rc.range_seek(fh->rc.user, uoff, 0, ulim);
     if (e != RC_NIL) {
@@ -750,8 +771,8 @@ extern "C" int32_t rc_hash_batch_with_nonce(rc_cipher* c, uint64_t n, const rc_r
                                             uint8_t* md5, int32_t* errs) {
   if (n == 0) return RC_NIL;
   if (!c || !srcs || !nonces || !md5 || !errs) return RC_ERR_INVALID;
-  xs_engine* e = engine();
-  if (!e) return RC_ERR_GPU;
+  xs_pool* pool = cipher_pool(c);
+  if (!pool) return RC_ERR_GPU;
   PinnedBuf buf;
   uint64_t pos = 0;
   std::vector<uint64_t> offs, lens;
@@ -784,7 +805,7 @@ extern "C" int32_t rc_hash_batch_with_nonce(rc_cipher* c, uint64_t n, const rc_r
   }
   if (idx.empty()) return RC_NIL;
   std::vector<uint8_t> dig(16 * idx.size());
-  if (xs_engine_seal_md5(e, c->data_key, idx.size(), ns.data(), offs.data(), lens.data(), buf.p, dig.data()) != XS_OK)
+  if (xs_pool_seal_md5(pool, c->data_key, idx.size(), ns.data(), offs.data(), lens.data(), buf.p, dig.data()) != XS_OK)
     return RC_ERR_GPU;
   for (size_t k = 0; k < idx.size(); k++) memcpy(md5 + 16 * idx[k], dig.data() + 16 * k, 16);
   return RC_NIL;

@@ -12,31 +12,28 @@
 //   lib/version Match / Remove / Add      lib/version/version.go
 //   pkcs7 Pad / Unpad                     backend/crypt/pkcs7/pkcs7.go:20-63
 //
+// Host code only: the GPU side (name engines, the EME launch, xs_eme_batch_dev) is in
+// names_gpu.cpp, so this file also builds into the CPU sanitizer harness (tests/native/).
+//
 // The reference encrypts one path segment per call; here a batch of names (a directory
 // listing, a sync's worth of object names) is split into segments on the host, every segment
 // that needs the block cipher is packed into one pinned buffer and transformed by a single
 // kernel launch, then the results are encoded and reassembled.  Outputs and errors (values
 // and which segment's error wins) are the reference's.
-#include <hip/hip_runtime.h>
-
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cctype>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "rc_internal.h"
-#include "xs_internal.h"
-
-namespace xs {
-hipError_t launch_eme(bool encrypt, const aes::EmeKey& key, const xs_name_desc* desc, uint64_t n, const uint8_t* src,
-                      uint8_t* dst, uint64_t buf_len, hipStream_t stream);
-}
 
 namespace {
 
@@ -169,13 +166,13 @@ Err dec_base32(const char* s0, size_t n0, std::vector<uint8_t>& out) {
     s += (ch >= 'a' && ch <= 'z') ? (char)(ch - 32) : ch;
   }
   s.append(equals, '=');
-  static int8_t map[256];
-  static bool init = false;
-  if (!init) {
-    memset(map, -1, sizeof map);
-    for (int i = 0; i < 32; i++) map[(uint8_t)kB32Hex[i]] = (int8_t)i;
-    init = true;
-  }
+  // built once, thread-safely (C++11 magic static): rc_names_run decodes from many threads
+  static const std::array<int8_t, 256> map = [] {
+    std::array<int8_t, 256> m;
+    m.fill(-1);
+    for (int i = 0; i < 32; i++) m[(uint8_t)kB32Hex[i]] = (int8_t)i;
+    return m;
+  }();
   const int64_t olen = (int64_t)s.size();
   size_t pos = 0;
   bool end = false;
@@ -229,13 +226,12 @@ void enc_base64(const uint8_t* p, size_t n, std::string& o) {
 // no padding, non-strict), CorruptInputError at the offending input byte.
 Err dec_base64(const char* s, size_t sn, std::vector<uint8_t>& out) {
   out.clear();
-  static int8_t map[256];
-  static bool init = false;
-  if (!init) {
-    memset(map, -1, sizeof map);
-    for (int i = 0; i < 64; i++) map[(uint8_t)kB64Url[i]] = (int8_t)i;
-    init = true;
-  }
+  static const std::array<int8_t, 256> map = [] {
+    std::array<int8_t, 256> m;
+    m.fill(-1);
+    for (int i = 0; i < 64; i++) m[(uint8_t)kB64Url[i]] = (int8_t)i;
+    return m;
+  }();
   size_t si = 0;
   while (si < sn) {
     uint8_t d[4] = {0};
@@ -542,51 +538,6 @@ Err deobfuscate(const rc_cipher* c, const std::string& ct, std::string* out) {
   return {};
 }
 
-// ------------------------------------------------------------------ GPU EME engine
-struct NameEngine {
-  std::mutex mu;
-  bool init = false, failed = false;
-  int device = 0;
-  hipStream_t s = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  uint8_t* d_buf = nullptr;
-  size_t d_cap = 0;
-  uint8_t* h_buf = nullptr;  // pinned
-  size_t h_cap = 0;
-};
-
-NameEngine g_names;
-
-bool ne_init(NameEngine& e) {
-  if (e.init) return true;
-  if (e.failed) return false;
-  if (const char* s = getenv("RCLONE_AMD_DEVICE")) e.device = atoi(s);
-  if (hipSetDevice(e.device) != hipSuccess || hipStreamCreateWithFlags(&e.s, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&e.ev0) != hipSuccess || hipEventCreate(&e.ev1) != hipSuccess) {
-    xs::set_error("name engine: no HIP device %d", e.device);
-    e.failed = true;
-    return false;
-  }
-  e.init = true;
-  return true;
-}
-
-bool ne_reserve(NameEngine& e, size_t bytes) {
-  if (bytes <= e.d_cap && bytes <= e.h_cap) return true;
-  size_t cap = e.d_cap ? e.d_cap : (1u << 20);
-  while (cap < bytes) cap *= 2;
-  if (e.d_buf) (void)hipFree(e.d_buf);
-  if (e.h_buf) (void)hipHostFree(e.h_buf);
-  e.d_buf = e.h_buf = nullptr;
-  e.d_cap = e.h_cap = 0;
-  if (hipMalloc(&e.d_buf, cap) != hipSuccess || hipHostMalloc(&e.h_buf, cap, hipHostMallocPortable) != hipSuccess) {
-    xs::set_error("name engine: cannot allocate %zu bytes", cap);
-    return false;
-  }
-  e.d_cap = e.h_cap = cap;
-  return true;
-}
-
 // A batch of segments for the block cipher: padded/decoded bytes packed at 16-aligned
 // offsets, then one H2D, one EME launch (in place), one D2H.
 struct SegBatch {
@@ -623,7 +574,8 @@ void parallel_for(size_t n, F f) {
   for (auto& t : th) t.join();
 }
 
-// All parts' segments in one pinned buffer -> one H2D, one EME launch (in place), one D2H.
+// All parts' segments in one pinned buffer -> one H2D, one EME launch (in place), one D2H
+// (names_gpu.cpp).
 int32_t run_eme(const rc_cipher* c, bool encrypt, std::vector<SegBatch*>& parts, double* ms) {
   *ms = 0;
   size_t nparts = parts.size();
@@ -634,37 +586,25 @@ int32_t run_eme(const rc_cipher* c, bool encrypt, std::vector<SegBatch*>& parts,
   }
   const size_t data_bytes = base[nparts], ndesc = dbase[nparts];
   if (ndesc == 0) return RC_NIL;
-  std::lock_guard<std::mutex> g(g_names.mu);
-  NameEngine& e = g_names;
-  if (!ne_init(e)) return RC_ERR_GPU;
   size_t desc_off = (data_bytes + 255) & ~(size_t)255;
   size_t total = desc_off + ndesc * sizeof(xs_name_desc);
-  if (hipSetDevice(e.device) != hipSuccess || !ne_reserve(e, total)) return RC_ERR_GPU;
-  xs_name_desc* hd = (xs_name_desc*)(e.h_buf + desc_off);
+  uint8_t* h = nullptr;
+  rcn::EmeDev* dev = rcn::eme_acquire(total, &h);
+  if (!dev) return RC_ERR_GPU;
+  xs_name_desc* hd = (xs_name_desc*)(h + desc_off);
   parallel_for(nparts, [&](size_t i) {
     const SegBatch& b = *parts[i];
-    memcpy(e.h_buf + base[i], b.data.data(), b.data.size());
+    memcpy(h + base[i], b.data.data(), b.data.size());
     for (size_t k = 0; k < b.desc.size(); k++) {
       hd[dbase[i] + k] = b.desc[k];
       hd[dbase[i] + k].off += base[i];
     }
   });
-  hipError_t err = hipMemcpyAsync(e.d_buf, e.h_buf, total, hipMemcpyHostToDevice, e.s);
-  if (err == hipSuccess) err = hipEventRecord(e.ev0, e.s);
-  if (err == hipSuccess)
-    err = xs::launch_eme(encrypt, c->eme, (const xs_name_desc*)(e.d_buf + desc_off), ndesc, e.d_buf, e.d_buf,
-                         data_bytes, e.s);
-  if (err == hipSuccess) err = hipEventRecord(e.ev1, e.s);
-  if (err == hipSuccess) err = hipMemcpyAsync(e.h_buf, e.d_buf, data_bytes, hipMemcpyDeviceToHost, e.s);
-  if (err == hipSuccess) err = hipStreamSynchronize(e.s);
-  if (err != hipSuccess) {
-    xs::set_error("name engine: %s", hipGetErrorString(err));
-    return RC_ERR_GPU;
-  }
-  float f = 0;
-  if (hipEventElapsedTime(&f, e.ev0, e.ev1) == hipSuccess) *ms = f;
-  parallel_for(nparts, [&](size_t i) { memcpy(parts[i]->data.data(), e.h_buf + base[i], parts[i]->data.size()); });
-  return RC_NIL;
+  int32_t rc = rcn::eme_run(dev, encrypt, c, desc_off, ndesc, data_bytes, total, ms);
+  if (rc == RC_NIL)
+    parallel_for(nparts, [&](size_t i) { memcpy(parts[i]->data.data(), h + base[i], parts[i]->data.size()); });
+  rcn::eme_release(dev);
+  return rc;
 }
 
 // ------------------------------------------------------------------ paths (flat, per chunk)
@@ -949,27 +889,10 @@ int32_t rc_name_decode(int32_t enc, const char* s, uint64_t n, uint8_t* out, uin
                        int64_t* err_arg) {
   std::vector<uint8_t> v;
   Err e = decode(enc, s ? s : "", s ? n : 0, v);
-  if (out) memcpy(out, v.data(), v.size() < cap ? v.size() : cap);
+  if (out && !v.empty()) memcpy(out, v.data(), v.size() < cap ? v.size() : cap);
   if (out_len) *out_len = v.size();
   if (err_arg) *err_arg = e.arg;
   return e.code;
-}
-
-int xs_eme_batch_dev(int encrypt, const uint8_t name_key[32], const uint8_t tweak[16], const xs_name_desc* d_desc,
-                     uint64_t n, const void* d_src, void* d_dst, uint64_t buf_len, void* stream) {
-  if (!name_key || !tweak || (n && (!d_desc || !d_src || !d_dst))) {
-    xs::set_error("xs_eme_batch_dev: null argument");
-    return XS_ERR_INVALID;
-  }
-  xs::aes::EmeKey k;
-  xs::aes::expand_key(name_key, tweak, &k);
-  hipError_t e = xs::launch_eme(encrypt != 0, k, d_desc, n, (const uint8_t*)d_src, (uint8_t*)d_dst, buf_len,
-                                (hipStream_t)stream);
-  if (e != hipSuccess) {
-    xs::set_error("eme launch: %s", hipGetErrorString(e));
-    return XS_ERR_HIP;
-  }
-  return XS_OK;
 }
 
 int32_t rc_names_run(rc_cipher* c, int32_t op, uint64_t n, const char* const* in, const uint64_t* in_len,

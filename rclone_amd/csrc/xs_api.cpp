@@ -8,14 +8,19 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
+#include "xs_host_md5.h"
 #include "xs_internal.h"
 
 namespace xs {
@@ -290,6 +295,7 @@ struct xs_engine {
     uint64_t blk0;  // first block within its combined batch
   };
   bool coalesce = true;
+  int host_md5_threads = -1;  // -1: the default (XS_MD5_HOST_THREADS or half the cores, <= 8); 0: GPU only
   bool zero_copy = true;  // pinned caller buffers go to the kernels directly (no staging copies)
   std::mutex qmu;
   std::condition_variable qcv;
@@ -316,6 +322,7 @@ struct xs_engine {
   std::vector<CSlot> cslots;
   uint64_t c_cap_blocks = 0, c_cap_bytes = 0;
   uint64_t st_batches = 0, st_reqs = 0, st_blocks = 0;
+  std::atomic<uint64_t> st_host_md5_objs{0}, st_host_md5_bytes{0};
   // grow-only buffers of xs_engine_seal_md5 (whole objects per group)
   struct HashBufs {
     uint8_t* d_plain = nullptr;
@@ -325,6 +332,8 @@ struct xs_engine {
     uint8_t* d_digest = nullptr;
     BlockKey* d_keys = nullptr;
     size_t plain_cap = 0, body_cap = 0, desc_cap = 0, mdesc_cap = 0, digest_cap = 0, keys_cap = 0;
+    hipStream_t aux = nullptr;        // wire-body D2H, overlapped with the MD5 lanes
+    hipEvent_t ev_sealed = nullptr;   // the group's seal is done (aux may copy the bodies)
   } hb;
 };
 
@@ -394,6 +403,11 @@ static void engine_free(xs_engine* e) {
   (void)hipFree(e->hb.d_mdesc);
   (void)hipFree(e->hb.d_digest);
   (void)hipFree(e->hb.d_keys);
+  if (e->hb.aux) {
+    (void)hipStreamSynchronize(e->hb.aux);
+    (void)hipStreamDestroy(e->hb.aux);
+  }
+  if (e->hb.ev_sealed) (void)hipEventDestroy(e->hb.ev_sealed);
   delete e;
 }
 
@@ -446,6 +460,16 @@ extern "C" xs_engine* xs_engine_create(int device, uint32_t batch_blocks, int ns
       engine_free(e);
       return nullptr;
     }
+    // hipHostMalloc does not promise zeroed memory: a stale word equal to the first sequence
+    // number would end the first spin wait before the kernel ran
+    memset(c.h_flag, 0, 64);
+    c.seq = 0;
+  }
+  if (hipStreamCreateWithFlags(&e->hb.aux, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&e->hb.ev_sealed, hipEventDisableTiming) != hipSuccess) {
+    set_error("xs_engine_create: stream/event creation failed");
+    engine_free(e);
+    return nullptr;
   }
   if (const char* v = getenv("XS_ENGINE_COALESCE")) e->coalesce = atoi(v) != 0;
   if (const char* v = getenv("XS_ENGINE_ZERO_COPY")) e->zero_copy = atoi(v) != 0;
@@ -626,7 +650,9 @@ static void nonce_plus(uint8_t out[24], const uint8_t n0[24], uint64_t x) {
 
 static NonceArg bounds_arg(uint64_t src_len, uint64_t dst_len);
 
-// Wait for fused batches by polling their completion word (XS_ENGINE_SPIN=0: the event only).
+// Wait for fused batches by polling their completion word (XS_ENGINE_SPIN=0: the event only),
+// for at most kSpinNs before falling back to a blocking event wait.
+constexpr int64_t kSpinNs = 200000;
 static bool spin_wait() {
   static const bool on = [] {
     const char* v = getenv("XS_ENGINE_SPIN");
@@ -835,12 +861,19 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
         // falling back to the event if the stream ends (or fails) without it
         bool seen = false;
         if (c.spin) {
+          // bounded: a fused batch takes tens of microseconds; past kSpinNs (a busy GPU) the
+          // leader blocks on the event instead of burning a core
+          const auto t0 = std::chrono::steady_clock::now();
           for (unsigned k = 1;; k++) {
             if (__atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) == c.seq) {
               seen = true;
               break;
             }
-            if ((k & 1023u) == 0 && hipEventQuery(c.done) != hipErrorNotReady) break;
+            __builtin_ia32_pause();
+            if ((k & 255u) == 0) {
+              if (hipEventQuery(c.done) != hipErrorNotReady) break;
+              if (std::chrono::steady_clock::now() - t0 > std::chrono::nanoseconds(kSpinNs)) break;
+            }
           }
         }
         hipError_t err = seen ? hipSuccess : hipEventSynchronize(c.done);
@@ -897,11 +930,134 @@ static uint64_t body_bytes(uint64_t plain_len) {
   return plain_len + nb * XS_BLOCK_HDR;
 }
 
+// ---- host MD5 for long objects
+// MD5 is one dependency chain per stream, so the GPU kernel runs one lane per object at
+// ~70 MB/s; one host core does ~0.5-1 GB/s.  A group of objects lasts as long as
+// its longest GPU lane, so the longest objects of a group are hashed on the host instead, over
+// the wire body the GPU sealed (crypt.put's tee hash, crypt.go:516-533, is the same bytes), by a
+// small worker pool that keeps running while the next group goes through the GPU.
+static double lane_md5_bps() {
+  static const double v = [] {
+    const char* e = getenv("XS_MD5_LANE_BPS");
+    return e ? atof(e) : 70e6;
+  }();
+  return v;
+}
+
+// One host core's MD5 rate, measured once (8 MiB, a few ms).
+static double host_md5_bps() {
+  static const double v = [] {
+    if (const char* e = getenv("XS_MD5_HOST_BPS")) return atof(e);
+    std::vector<uint8_t> b((size_t)8 << 20, 0x5a);
+    uint8_t out[16];
+    const auto t0 = std::chrono::steady_clock::now();
+    HostMd5 m;
+    m.update(b.data(), b.size());
+    m.final(out);
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return s > 0 ? (double)b.size() / s : 500e6;
+  }();
+  return v;
+}
+
+static int host_md5_threads_default() {
+  if (const char* e = getenv("XS_MD5_HOST_THREADS")) return std::max(0, atoi(e));
+  const unsigned hc = std::thread::hardware_concurrency();
+  return (int)std::max(1u, std::min(8u, hc ? hc / 2 : 1u));
+}
+
+constexpr uint64_t kHostMd5Min = 1ull << 20;  // below this an object stays on its GPU lane
+
+// Which objects of a group go to the host (route[k] = 1): take the longest first while the host
+// pool's makespan stays below that object's GPU lane time, i.e. while moving it shortens the
+// group (the group's GPU MD5 time is then set by the longest object left on the GPU).
+static void route_host_md5(const uint64_t* wire_len, size_t n, int threads, std::vector<uint8_t>& route) {
+  route.assign(n, 0);
+  if (threads <= 0 || n == 0) return;
+  std::vector<size_t> order;
+  for (size_t k = 0; k < n; k++)
+    if (wire_len[k] >= kHostMd5Min) order.push_back(k);
+  if (order.empty()) return;
+  std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return wire_len[a] > wire_len[b]; });
+  const double hb = host_md5_bps(), lb = lane_md5_bps();
+  double sum = 0, mx = 0;
+  for (size_t k : order) {
+    const double L = (double)wire_len[k];
+    const double nsum = sum + L, nmx = std::max(mx, L);
+    const double host_t = std::max(nmx, nsum / threads) / hb;
+    if (host_t >= L / lb) break;
+    route[k] = 1;
+    sum = nsum;
+    mx = nmx;
+  }
+}
+
+namespace {
+struct HostMd5Pool {
+  struct Job {
+    uint8_t prefix[32];
+    const uint8_t* body;
+    uint64_t len;
+    uint8_t* out;
+    std::unique_ptr<uint8_t[]> own;  // body copy when the caller gets no wire bodies back
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Job> jobs;
+  size_t next = 0;
+  bool closing = false;
+  std::vector<std::thread> th;
+  uint64_t bytes = 0, count = 0;
+
+  void push(Job&& j, int max_threads) {
+    std::lock_guard<std::mutex> g(mu);
+    bytes += j.len;
+    count++;
+    jobs.push_back(std::move(j));
+    if ((int)th.size() < max_threads && th.size() < jobs.size() - next) th.emplace_back([this] { work(); });
+    cv.notify_one();
+  }
+  void work() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return next < jobs.size() || closing; });
+      if (next >= jobs.size()) return;
+      Job& j = jobs[next++];  // jobs only grow; index stays valid, element moves on realloc
+      uint8_t prefix[32];
+      memcpy(prefix, j.prefix, 32);
+      const uint8_t* body = j.own ? j.own.get() : j.body;
+      const uint64_t len = j.len;
+      uint8_t* out = j.out;
+      std::unique_ptr<uint8_t[]> own = std::move(j.own);
+      lk.unlock();
+      HostMd5 m;
+      m.update(prefix, 32);
+      m.update(body, len);
+      m.final(out);
+      own.reset();
+      lk.lock();
+    }
+  }
+  void finish() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      closing = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+    th.clear();
+  }
+  ~HostMd5Pool() { finish(); }
+};
+}  // namespace
+
 // Seal + MD5 of whole objects in groups of ~budget plaintext bytes; with `body` the wire
 // bodies also come back (packed: object i at xs_put_body_offset of i, one D2H per group).
+// host_threads > 0 lets the longest objects of a group be hashed on the host (route_host_md5).
 static int seal_md5_impl(xs_engine* e, const uint8_t key[32], uint64_t nobj, const uint8_t* nonces,
                          const uint64_t* offs, const uint64_t* lens, const void* plain, uint8_t* md5,
-                         uint8_t* body) {
+                         uint8_t* body, int host_threads, uint64_t* host_routed) {
+  if (host_routed) *host_routed = 0;
   if (nobj == 0) return XS_OK;
   if (!e || !key || !nonces || !offs || !lens || !md5) {
     set_error("xs_engine_seal_md5: null argument");
@@ -919,11 +1075,14 @@ static int seal_md5_impl(xs_engine* e, const uint8_t key[32], uint64_t nobj, con
   if (hipSetDevice(e->device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
   hipStream_t st = e->slots[0].s;
   auto& hb = e->hb;
+  HostMd5Pool host;  // joined (every digest written) before this function returns
   // groups of whole objects, ~budget plaintext bytes each (MD5 is sequential per object)
   // large groups: the MD5 of a group takes as long as its largest object (one lane each)
   const uint64_t budget = std::max<uint64_t>((uint64_t)e->batch * XS_BLOCK_DATA * 16, 4096ull << 20);
   std::vector<xs_block_desc> desc;
   std::vector<xs_md5_desc> mdesc;
+  std::vector<uint64_t> wlen, gpu_obj, host_obj;
+  std::vector<uint8_t> route, dig;
   uint64_t o0 = 0, body_pos = 0;
   while (o0 < nobj) {
     uint64_t o1 = o0, lo = UINT64_MAX, hi = 0, bsum = 0, nblk = 0;
@@ -937,17 +1096,30 @@ static int seal_md5_impl(xs_engine* e, const uint8_t key[32], uint64_t nobj, con
       o1++;
     }
     const uint64_t span = hi > lo ? hi - lo : 0, ng = o1 - o0;
+    wlen.resize(ng);
+    for (uint64_t i = o0; i < o1; i++) wlen[i - o0] = body_bytes(lens[i]);
+    route_host_md5(wlen.data(), ng, host_threads, route);
     desc.clear();
-    mdesc.assign(ng, xs_md5_desc{});
+    mdesc.clear();
+    gpu_obj.clear();
+    host_obj.clear();
     uint64_t w = 0;
+    std::vector<uint64_t> wpos(ng);
     for (uint64_t i = o0; i < o1; i++) {
       const uint64_t nb = (lens[i] + XS_BLOCK_DATA - 1) / XS_BLOCK_DATA;
-      xs_md5_desc& m = mdesc[i - o0];
-      m.off = w;
-      m.len = body_bytes(lens[i]);
-      memcpy(m.prefix, magic, 8);
-      memcpy(m.prefix + 8, nonces + 24 * i, 24);
-      m.prefix_len = 32;
+      wpos[i - o0] = w;
+      if (route[i - o0]) {
+        host_obj.push_back(i);
+      } else {
+        xs_md5_desc m{};
+        m.off = w;
+        m.len = wlen[i - o0];
+        memcpy(m.prefix, magic, 8);
+        memcpy(m.prefix + 8, nonces + 24 * i, 24);
+        m.prefix_len = 32;
+        mdesc.push_back(m);
+        gpu_obj.push_back(i);
+      }
       for (uint64_t j = 0; j < nb; j++) {
         xs_block_desc d{};
         d.src_off = offs[i] - lo + j * XS_BLOCK_DATA;
@@ -958,11 +1130,13 @@ static int seal_md5_impl(xs_engine* e, const uint8_t key[32], uint64_t nobj, con
         nonce_add_host(d.nonce, j);
         desc.push_back(d);
       }
-      w += (m.len + 15) & ~15ull;
+      w += (wlen[i - o0] + 15) & ~15ull;
     }
+    const uint64_t ngpu = mdesc.size();
     if (!grow(&hb.d_plain, &hb.plain_cap, span) || !grow(&hb.d_body, &hb.body_cap, bsum) ||
         !grow(&hb.d_desc, &hb.desc_cap, nblk * sizeof(xs_block_desc)) ||
-        !grow(&hb.d_mdesc, &hb.mdesc_cap, ng * sizeof(xs_md5_desc)) || !grow(&hb.d_digest, &hb.digest_cap, ng * 16) ||
+        !grow(&hb.d_mdesc, &hb.mdesc_cap, std::max<uint64_t>(ngpu, 1) * sizeof(xs_md5_desc)) ||
+        !grow(&hb.d_digest, &hb.digest_cap, std::max<uint64_t>(ngpu, 1) * 16) ||
         !grow((uint8_t**)&hb.d_keys, &hb.keys_cap, nblk * sizeof(BlockKey))) {
       set_error("xs_engine_seal_md5: device allocation failed");
       return XS_ERR_HIP;
@@ -971,8 +1145,8 @@ static int seal_md5_impl(xs_engine* e, const uint8_t key[32], uint64_t nobj, con
     if (span) err = hipMemcpyAsync(hb.d_plain, (const uint8_t*)plain + lo, span, hipMemcpyHostToDevice, st);
     if (err == hipSuccess && nblk)
       err = hipMemcpyAsync(hb.d_desc, desc.data(), nblk * sizeof(xs_block_desc), hipMemcpyHostToDevice, st);
-    if (err == hipSuccess)
-      err = hipMemcpyAsync(hb.d_mdesc, mdesc.data(), ng * sizeof(xs_md5_desc), hipMemcpyHostToDevice, st);
+    if (err == hipSuccess && ngpu)
+      err = hipMemcpyAsync(hb.d_mdesc, mdesc.data(), ngpu * sizeof(xs_md5_desc), hipMemcpyHostToDevice, st);
     if (err != hipSuccess) return hip_fail(err, "H2D");
     if (nblk) {
       err = launch_keygen(2, key_arg(key), bounds_arg(span, bsum), 0, 0, nblk, (const xs_block_desc*)hb.d_desc,
@@ -981,23 +1155,68 @@ static int seal_md5_impl(xs_engine* e, const uint8_t key[32], uint64_t nobj, con
       err = launch_crypt(true, hb.d_keys, nblk, hb.d_plain, hb.d_body, nullptr, st);
       if (err != hipSuccess) return hip_fail(err, "seal");
     }
-    err = launch_md5((const xs_md5_desc*)hb.d_mdesc, ng, hb.d_body, bsum, hb.d_digest, nullptr, st);
-    if (err != hipSuccess) return hip_fail(err, "md5");
-    err = hipMemcpyAsync(md5 + 16 * o0, hb.d_digest, ng * 16, hipMemcpyDeviceToHost, st);
-    if (err == hipSuccess && body && w) err = hipMemcpyAsync(body + body_pos, hb.d_body, w, hipMemcpyDeviceToHost, st);
+    // the wire bodies (all of them for put_batch, the host-routed ones otherwise) leave on the
+    // aux stream while the MD5 lanes run on st; the host pool starts as soon as they have landed
+    hipStream_t ax = hb.aux;
+    if (err == hipSuccess) err = hipEventRecord(hb.ev_sealed, st);
+    if (err == hipSuccess) err = hipStreamWaitEvent(ax, hb.ev_sealed, 0);
+    std::vector<std::unique_ptr<uint8_t[]>> own(host_obj.size());
+    if (!body) {
+      for (size_t k = 0; k < host_obj.size() && err == hipSuccess; k++) {
+        const uint64_t i = host_obj[k], len = wlen[i - o0];
+        own[k].reset(new (std::nothrow) uint8_t[len ? len : 1]);
+        if (!own[k]) {
+          set_error("xs_engine_seal_md5: host allocation of %llu bytes failed", (unsigned long long)len);
+          return XS_ERR_NOMEM;
+        }
+        if (len) err = hipMemcpyAsync(own[k].get(), hb.d_body + wpos[i - o0], len, hipMemcpyDeviceToHost, ax);
+      }
+    } else if (w && err == hipSuccess) {
+      err = hipMemcpyAsync(body + body_pos, hb.d_body, w, hipMemcpyDeviceToHost, ax);
+    }
     if (err != hipSuccess) return hip_fail(err, "D2H");
-    body_pos += w;
+    if (ngpu) {
+      err = launch_md5((const xs_md5_desc*)hb.d_mdesc, ngpu, hb.d_body, bsum, hb.d_digest, nullptr, st);
+      if (err != hipSuccess) return hip_fail(err, "md5");
+      dig.resize(16 * ngpu);
+      err = hipMemcpyAsync(dig.data(), hb.d_digest, ngpu * 16, hipMemcpyDeviceToHost, st);
+      if (err != hipSuccess) return hip_fail(err, "D2H");
+    }
+    err = hipStreamSynchronize(ax);
+    if (err != hipSuccess) return hip_fail(err, "engine aux stream");
+    for (size_t k = 0; k < host_obj.size(); k++) {
+      const uint64_t i = host_obj[k];
+      HostMd5Pool::Job j;
+      memcpy(j.prefix, magic, 8);
+      memcpy(j.prefix + 8, nonces + 24 * i, 24);
+      j.body = body ? body + body_pos + wpos[i - o0] : nullptr;
+      j.len = wlen[i - o0];
+      j.out = md5 + 16 * i;
+      j.own = std::move(own[k]);
+      host.push(std::move(j), host_threads);
+    }
     // the host-side descriptor vectors are reused next group: wait for this group's copies
     err = hipStreamSynchronize(st);
     if (err != hipSuccess) return hip_fail(err, "engine stream");
+    for (uint64_t k = 0; k < ngpu; k++) memcpy(md5 + 16 * gpu_obj[k], dig.data() + 16 * k, 16);
+    body_pos += w;
     o0 = o1;
   }
+  host.finish();
+  if (host_routed) *host_routed = host.count;
+  e->st_host_md5_objs += host.count;
+  e->st_host_md5_bytes += host.bytes;
   return XS_OK;
 }
 
 extern "C" int xs_engine_seal_md5(xs_engine* e, const uint8_t key[32], uint64_t nobj, const uint8_t* nonces,
                                   const uint64_t* offs, const uint64_t* lens, const void* plain, uint8_t* md5) {
-  return seal_md5_impl(e, key, nobj, nonces, offs, lens, plain, md5, nullptr);
+  if (!e) {
+    set_error("xs_engine_seal_md5: null engine");
+    return XS_ERR_INVALID;
+  }
+  return seal_md5_impl(e, key, nobj, nonces, offs, lens, plain, md5, nullptr,
+                       e->host_md5_threads >= 0 ? e->host_md5_threads : host_md5_threads_default(), nullptr);
 }
 
 extern "C" uint64_t xs_put_body_bytes(uint64_t nobj, const uint64_t* lens) {
@@ -1013,5 +1232,163 @@ extern "C" int xs_engine_put_batch(xs_engine* e, const uint8_t key[32], uint64_t
     set_error("xs_engine_put_batch: null body");
     return XS_ERR_INVALID;
   }
-  return seal_md5_impl(e, key, nobj, nonces, offs, lens, plain, md5, (uint8_t*)body);
+  if (!e) {
+    set_error("xs_engine_put_batch: null engine");
+    return XS_ERR_INVALID;
+  }
+  return seal_md5_impl(e, key, nobj, nonces, offs, lens, plain, md5, (uint8_t*)body,
+                       e->host_md5_threads >= 0 ? e->host_md5_threads : host_md5_threads_default(), nullptr);
+}
+
+extern "C" void xs_engine_set_host_md5(xs_engine* e, int threads) {
+  if (e) e->host_md5_threads = threads;
+}
+
+extern "C" void xs_engine_md5_stats(xs_engine* e, uint64_t out[2]) {
+  if (!e || !out) return;
+  out[0] = e->st_host_md5_objs.load();
+  out[1] = e->st_host_md5_bytes.load();
+}
+
+// ---------------------------------------------------------------- multi-device engine pool
+// One rclone process runs many transfers and checkers at once (fs/sync/sync.go:544
+// startTransfers, --transfers / --checkers); objects are independent, so a process spreads them
+// over every GPU of the node: object streams take engines round-robin (xs_pool_next), batched
+// put / cryptcheck calls split their objects into contiguous byte-balanced ranges, one per
+// engine, run concurrently.  Several engines may sit on one device (a list like "0,0,0,0").
+namespace xs {
+std::vector<int> default_devices() {
+  std::vector<int> v;
+  const char* list = getenv("RCLONE_AMD_DEVICES");
+  if (list && *list) {
+    const char* p = list;
+    while (*p) {
+      char* end = nullptr;
+      const long d = strtol(p, &end, 10);
+      if (end == p) break;
+      v.push_back((int)d);
+      p = end;
+      while (*p == ',' || *p == ' ') p++;
+    }
+    if (!v.empty()) return v;
+  }
+  if (const char* one = getenv("RCLONE_AMD_DEVICE")) {
+    v.push_back(atoi(one));
+    return v;
+  }
+  const int n = xs_device_count();
+  for (int d = 0; d < n; d++) v.push_back(d);
+  return v;
+}
+}  // namespace xs
+
+struct xs_pool {
+  std::vector<xs_engine*> engines;
+  std::atomic<uint64_t> rr{0};
+};
+
+extern "C" xs_pool* xs_pool_create(const int* devices, int ndevices, uint32_t batch_blocks, int nslots) {
+  std::vector<int> devs;
+  if (devices && ndevices > 0) devs.assign(devices, devices + ndevices);
+  else devs = default_devices();
+  if (devs.empty()) {
+    set_error("xs_pool_create: no HIP device");
+    return nullptr;
+  }
+  xs_pool* p = new xs_pool();
+  for (int d : devs) {
+    xs_engine* e = xs_engine_create(d, batch_blocks, nslots);
+    if (!e) {
+      const std::string msg = xs_last_error();
+      for (auto* x : p->engines) xs_engine_destroy(x);
+      delete p;
+      set_error("xs_pool_create: %s", msg.c_str());
+      return nullptr;
+    }
+    p->engines.push_back(e);
+  }
+  return p;
+}
+
+extern "C" void xs_pool_destroy(xs_pool* p) {
+  if (!p) return;
+  for (auto* e : p->engines) xs_engine_destroy(e);
+  delete p;
+}
+
+extern "C" int xs_pool_size(const xs_pool* p) { return p ? (int)p->engines.size() : 0; }
+
+extern "C" xs_engine* xs_pool_engine(xs_pool* p, int i) {
+  if (!p || i < 0 || i >= (int)p->engines.size()) return nullptr;
+  return p->engines[i];
+}
+
+extern "C" xs_engine* xs_pool_next(xs_pool* p) {
+  if (!p || p->engines.empty()) return nullptr;
+  return p->engines[p->rr.fetch_add(1) % p->engines.size()];
+}
+
+// Objects [0, nobj) split into k contiguous ranges of about equal plaintext bytes, one engine
+// each, run on their own threads; the first failure's message is passed to the caller's thread.
+static int pool_seal_md5(xs_pool* p, const uint8_t key[32], uint64_t nobj, const uint8_t* nonces,
+                         const uint64_t* offs, const uint64_t* lens, const void* plain, uint8_t* md5, uint8_t* body) {
+  if (!p || p->engines.empty()) {
+    set_error("xs_pool: no engines");
+    return XS_ERR_INVALID;
+  }
+  if (nobj == 0) return XS_OK;
+  if (!key || !nonces || !offs || !lens || !md5) {
+    set_error("xs_pool_seal_md5: null argument");
+    return XS_ERR_INVALID;
+  }
+  const uint64_t k = std::min<uint64_t>(p->engines.size(), nobj);
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < nobj; i++) total += lens[i] + 1;  // +1: empty objects still count
+  std::vector<uint64_t> cut{0};
+  uint64_t acc = 0;
+  for (uint64_t i = 0; i < nobj && cut.size() < k; i++) {
+    acc += lens[i] + 1;
+    if (acc * k >= total * cut.size() && i + 1 < nobj) cut.push_back(i + 1);
+  }
+  cut.push_back(nobj);
+  const int ht = host_md5_threads_default();
+  const int per = ht > 0 ? std::max(1, ht / (int)(cut.size() - 1)) : 0;
+  std::vector<int> rc(cut.size() - 1, XS_OK);
+  std::vector<std::string> msg(cut.size() - 1);
+  std::vector<std::thread> th;
+  uint64_t bpos = 0;
+  const uint64_t first = p->rr.fetch_add(cut.size() - 1);  // distinct engines for the ranges
+  for (size_t r = 0; r + 1 < cut.size(); r++) {
+    const uint64_t a = cut[r], b = cut[r + 1];
+    uint8_t* rb = body ? body + bpos : nullptr;
+    for (uint64_t i = a; i < b; i++) bpos += (body_bytes(lens[i]) + 15) & ~15ull;
+    xs_engine* e = p->engines[(first + r) % p->engines.size()];
+    th.emplace_back([&, r, a, b, rb, e] {
+      rc[r] = seal_md5_impl(e, key, b - a, nonces + 24 * a, offs + a, lens + a, plain, md5 + 16 * a, rb,
+                            e->host_md5_threads >= 0 ? e->host_md5_threads : per, nullptr);
+      if (rc[r] != XS_OK) msg[r] = xs_last_error();
+    });
+  }
+  for (auto& t : th) t.join();
+  for (size_t r = 0; r < rc.size(); r++)
+    if (rc[r] != XS_OK) {
+      set_error("%s", msg[r].c_str());
+      return rc[r];
+    }
+  return XS_OK;
+}
+
+extern "C" int xs_pool_seal_md5(xs_pool* p, const uint8_t key[32], uint64_t nobj, const uint8_t* nonces,
+                                const uint64_t* offs, const uint64_t* lens, const void* plain, uint8_t* md5) {
+  return pool_seal_md5(p, key, nobj, nonces, offs, lens, plain, md5, nullptr);
+}
+
+extern "C" int xs_pool_put_batch(xs_pool* p, const uint8_t key[32], uint64_t nobj, const uint8_t* nonces,
+                                 const uint64_t* offs, const uint64_t* lens, const void* plain, void* body,
+                                 uint8_t* md5) {
+  if (nobj && !body) {
+    set_error("xs_pool_put_batch: null body");
+    return XS_ERR_INVALID;
+  }
+  return pool_seal_md5(p, key, nobj, nonces, offs, lens, plain, md5, (uint8_t*)body);
 }

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/rclone_crypt_gpu.h"
 
 namespace xs {
@@ -64,6 +66,7 @@ hipError_t launch_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t f
                        hipStream_t stream);
 
 void set_error(const char* fmt, ...);
+std::vector<int> default_devices();  // see rc_internal.h
 #ifdef XS_CLOCK_PROBE
 void probe_read(unsigned long long* host, size_t n);
 #endif
