@@ -164,9 +164,10 @@ void xs_engine_stats(xs_engine *e, uint64_t out[3]);
  * longest objects of a group are hashed on host cores over the GPU-sealed wire body when that
  * shortens the group (one GPU lane does ~70 MB/s, one core ~10x that).  threads = host MD5
  * workers (0 = every object on the GPU; default XS_MD5_HOST_THREADS or half the cores, <= 8).
- * out[0] = objects hashed on the host so far, out[1] = their wire bytes. */
+ * out[0] = objects hashed on the host so far, out[1] = their wire bytes, out[2] = all objects
+ * sealed + hashed by this engine. */
 void xs_engine_set_host_md5(xs_engine *e, int threads);
-void xs_engine_md5_stats(xs_engine *e, uint64_t out[2]);
+void xs_engine_md5_stats(xs_engine *e, uint64_t out[3]);
 
 /* Multi-device engine pool: one process spreads its objects over several GPUs (or several
  * engines per GPU).  devices = HIP device ids, repeats allowed ("0,0,0,0" = four engines on
@@ -242,13 +243,18 @@ void rc_cipher_set_pass_bad_blocks(rc_cipher *c, int32_t pass); /* setPassBadBlo
 void rc_cipher_set_rand(rc_cipher *c, rc_reader rand);           /* c.cryptoRand */
 /* Read-ahead of encrypters/decrypters.  The first refill of a stream, and the first after a
  * seek, reads first_blocks blocks (default 1: exactly what encrypter.Read / fillBuffer read,
- * cipher.go:726-741, :862-898); each later refill doubles, up to batch_blocks per GPU submission
- * (default 64 = 4 MiB).  first_blocks = 0: every refill reads batch_blocks. */
+ * cipher.go:726-741, :862-898); later refills grow up to batch_blocks per GPU submission
+ * (default 64 = 4 MiB): by `factor` each refill, or with factor 0 (default) by doubling while
+ * the source is slow and straight to batch_blocks once a refill read faster than 2 GB/s.
+ * first_blocks = 0: every refill reads batch_blocks. */
 void rc_cipher_set_batch_blocks(rc_cipher *c, uint32_t blocks);
 void rc_cipher_set_readahead(rc_cipher *c, uint32_t first_blocks);
+void rc_cipher_set_readahead_growth(rc_cipher *c, uint32_t factor);
 /* GPU engines used by this cipher's handles and batches (NULL: the process-wide pool over
  * RCLONE_AMD_DEVICES / RCLONE_AMD_DEVICE / every device).  The pool must outlive the cipher. */
 void rc_cipher_set_pool(rc_cipher *c, xs_pool *pool);
+/* The process-wide pool (created on first use; NULL with xs_last_error when no device). */
+xs_pool *rc_default_pool(void);
 void rc_cipher_free(rc_cipher *c);
 
 int64_t rc_encrypted_size(int64_t size);               /* EncryptedSize :1121 */

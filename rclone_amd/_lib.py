@@ -85,7 +85,9 @@ _SIGS = [
     ("rc_cipher_set_rand", None, [vp, RcReader]),
     ("rc_cipher_set_batch_blocks", None, [vp, ctypes.c_uint32]),
     ("rc_cipher_set_readahead", None, [vp, ctypes.c_uint32]),
+    ("rc_cipher_set_readahead_growth", None, [vp, ctypes.c_uint32]),
     ("rc_cipher_set_pool", None, [vp, vp]),
+    ("rc_default_pool", vp, []),
     ("rc_cipher_free", None, [vp]),
     ("rc_encrypted_size", i64, [i64]),
     ("rc_decrypted_size", i64, [i64, ctypes.POINTER(i32)]),

@@ -277,6 +277,37 @@ class Cipher(NameCipherMixin):
         _lib.lib().rc_cipher_set_batch_blocks(self._h, int(v))
 
     @property
+    def readahead(self):
+        """Blocks read by the first refill of a stream / after a seek (rc_cipher_set_readahead;
+        1 = the reference's one block, doubling up to batch_blocks after that; 0 = full batches)."""
+        return getattr(self, "_ra", 1)
+
+    @readahead.setter
+    def readahead(self, v):
+        self._ra = int(v)
+        _lib.lib().rc_cipher_set_readahead(self._h, int(v))
+
+    @property
+    def readahead_growth(self):
+        """Refill growth factor (rc_cipher_set_readahead_growth; 0 = adaptive to the source rate)."""
+        return getattr(self, "_rag", 0)
+
+    @readahead_growth.setter
+    def readahead_growth(self, v):
+        self._rag = int(v)
+        _lib.lib().rc_cipher_set_readahead_growth(self._h, int(v))
+
+    @property
+    def pool(self):
+        return getattr(self, "_pool", None)
+
+    @pool.setter
+    def pool(self, p):
+        """Bind this cipher's handles and batches to an EnginePool (None: the process pool)."""
+        self._pool = p
+        _lib.lib().rc_cipher_set_pool(self._h, p.handle if p is not None else None)
+
+    @property
     def crypto_rand(self):
         return self._rand
 
@@ -344,6 +375,41 @@ class Cipher(NameCipherMixin):
         nonce = d.nonce
         d.close()
         return self.compute_hash_with_nonce(nonce, src)
+
+
+class EnginePool:
+    """xs_pool: GPU engines over a device list (repeats allowed: several engines on one device);
+    None -> RCLONE_AMD_DEVICES / RCLONE_AMD_DEVICE / every device."""
+
+    def __init__(self, devices=None, batch_blocks: int = 256, slots: int = 3):
+        L = _lib.lib()
+        if devices:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            self.handle = L.xs_pool_create(arr, len(devices), batch_blocks, slots)
+        else:
+            self.handle = L.xs_pool_create(None, 0, batch_blocks, slots)
+        if not self.handle:
+            raise RuntimeError("xs_pool_create: " + _lib.last_error())
+
+    def __len__(self):
+        return _lib.lib().xs_pool_size(self.handle)
+
+    def engine(self, i):
+        return _lib.lib().xs_pool_engine(self.handle, i)
+
+    def stats(self):
+        """Per engine: (combined batches, requests, blocks) of its coalescing queue."""
+        out = []
+        for i in range(len(self)):
+            a = (ctypes.c_uint64 * 3)()
+            _lib.lib().xs_engine_stats(self.engine(i), a)
+            out.append(tuple(a))
+        return out
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.lib().xs_pool_destroy(self.handle)
+            self.handle = None
 
 
 class Encrypter:

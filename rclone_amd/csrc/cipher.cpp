@@ -22,6 +22,7 @@
 #include <cerrno>
 #include <cstdlib>
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -83,6 +84,12 @@ xs_pool* process_pool() {
 }
 
 xs_pool* cipher_pool(const rc_cipher* c) { return c->pool ? c->pool : process_pool(); }
+
+}  // namespace
+
+extern "C" xs_pool* rc_default_pool(void) { return process_pool(); }
+
+namespace {
 
 // Pinned staging pool -- the counterpart of the reference's Cipher.buffers sync.Pool
 // (cipher.go:179, :255-262): handles come and go per object, and hipHostMalloc/hipHostFree
@@ -200,6 +207,7 @@ extern "C" void rc_cipher_set_pass_bad_blocks(rc_cipher* c, int32_t pass) { c->p
 extern "C" void rc_cipher_set_rand(rc_cipher* c, rc_reader rand) { c->rand = rand; }
 extern "C" void rc_cipher_set_batch_blocks(rc_cipher* c, uint32_t blocks) { c->batch_blocks = blocks ? blocks : 1; }
 extern "C" void rc_cipher_set_readahead(rc_cipher* c, uint32_t first_blocks) { c->first_blocks = first_blocks; }
+extern "C" void rc_cipher_set_readahead_growth(rc_cipher* c, uint32_t factor) { c->growth = factor == 1 ? 2 : factor; }
 extern "C" void rc_cipher_set_pool(rc_cipher* c, xs_pool* pool) { c->pool = pool; }
 extern "C" void rc_cipher_free(rc_cipher* c) { delete c; }
 
@@ -311,15 +319,25 @@ extern "C" const char* rc_error_string(int32_t e) {
 
 // ---------------------------------------------------------------- encrypter
 // Read-ahead: the first refill of a stream (and the first after a seek) reads exactly one block,
-// as encrypter.Read / fillBuffer do (cipher.go:726-741, :862-898); each later refill doubles, up
-// to the cipher's batch_blocks, so a slow or streaming source sees the reference's first-byte
-// behaviour and a long one reaches full GPU batches after a few refills.
-static uint32_t next_batch(const rc_cipher* c, uint32_t* grow) {
+// as encrypter.Read / fillBuffer do (cipher.go:726-741, :862-898), so a slow or streaming source
+// sees the reference's first-byte behaviour.  Later refills grow up to the cipher's batch_blocks:
+// by the cipher's growth factor, or (growth 0, the default) by doubling while the source is slow
+// and straight to full batches once a refill shows a fast source (memory, page cache: > 2 GB/s),
+// where every extra GPU round trip would only cost throughput.
+constexpr double kFastSourceBps = 2e9;
+
+static uint32_t next_batch(const rc_cipher* c, uint32_t grow) {
   const uint32_t cap = c->batch_blocks;
-  if (*grow == 0) *grow = c->first_blocks ? c->first_blocks : cap;  // 0: full batches at once
-  const uint32_t n = std::min(*grow, cap);
-  *grow = (uint32_t)std::min<uint64_t>((uint64_t)*grow * 2, cap);
-  return n;
+  if (grow == 0) grow = c->first_blocks ? c->first_blocks : cap;  // first_blocks 0: full batches at once
+  return std::min(grow, cap);
+}
+
+static uint32_t grow_batch(const rc_cipher* c, uint32_t used, int64_t bytes, std::chrono::steady_clock::duration t) {
+  const uint64_t cap = c->batch_blocks;
+  uint64_t next = (uint64_t)used * (c->growth ? c->growth : 2);
+  if (c->growth == 0 && bytes > 0 && std::chrono::duration<double>(t).count() * kFastSourceBps < (double)bytes)
+    next = cap;
+  return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(next, 1), cap);
 }
 
 struct rc_encrypter {
@@ -395,10 +413,11 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
   if (fh->buf_index >= fh->buf_size) {
     // refill: ReadFill block by block exactly as encrypter.Read would, up to next_batch blocks
     fh->in_hdr = false;
-    const uint32_t batch = next_batch(fh->c, &fh->grow);
+    const uint32_t batch = next_batch(fh->c, fh->grow);
     if (!fh->plain.ensure((size_t)fh->c->batch_blocks * kBlockData) ||
         !fh->wire.ensure((size_t)fh->c->batch_blocks * kBlockSize))
       return enc_finish(fh, RC_ERR_GPU, err);
+    const auto t0 = std::chrono::steady_clock::now();
     int64_t total = 0;
     uint32_t nb = 0;
     int32_t first_err = RC_NIL;
@@ -416,6 +435,7 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
       }
     }
     if (nb == 0) return enc_finish(fh, first_err, err);
+    fh->grow = grow_batch(fh->c, batch, total, std::chrono::steady_clock::now() - t0);
     if (!fh->eng) fh->eng = xs_pool_next(cipher_pool(fh->c));
     if (!fh->eng ||
         xs_engine_seal(fh->eng, fh->c->data_key, fh->nonce, 0, fh->plain.p, (uint64_t)total, fh->wire.p) != XS_OK)
@@ -503,9 +523,10 @@ static int32_t dec_close_locked(rc_decrypter* fh) {
 // the GPU.  Errors are not returned here; they are queued at the block position where
 // fillBuffer (cipher.go:862-898) would return them.
 static int32_t dec_read_batch(rc_decrypter* fh, uint32_t want) {
-  const uint32_t ra = next_batch(fh->c, &fh->grow);
+  const uint32_t ra = next_batch(fh->c, fh->grow);
   if (want == 0 || want > ra) want = ra;
   if (!dec_alloc(fh)) return RC_ERR_GPU;
+  const auto t0 = std::chrono::steady_clock::now();
   fh->blen.assign(want, 0);
   fh->berr.assign(want, RC_NIL);
   fh->nblk = fh->cur = 0;
@@ -535,6 +556,7 @@ static int32_t dec_read_batch(rc_decrypter* fh, uint32_t want) {
   }
   fh->nblk = nb;
   if (nb == 0) return RC_NIL;
+  fh->grow = grow_batch(fh->c, ra, total, std::chrono::steady_clock::now() - t0);
   if (!fh->eng) fh->eng = xs_pool_next(cipher_pool(fh->c));
   if (!fh->eng || xs_engine_open(fh->eng, fh->c->data_key, fh->nonce, 0, fh->wire.p, (uint64_t)total, fh->plain.p,
                                  fh->okb.p) != XS_OK) {

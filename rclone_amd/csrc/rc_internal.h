@@ -28,6 +28,7 @@ struct rc_cipher {
   rc_reader rand{};  // c.cryptoRand; read == NULL -> OS random
   uint32_t batch_blocks = 64;  // read-ahead cap per GPU submission (rc_cipher_set_batch_blocks)
   uint32_t first_blocks = 1;   // first refill of a stream / after a seek (rc_cipher_set_readahead)
+  uint32_t growth = 0;         // refill growth factor; 0 = adaptive (rc_cipher_set_readahead_growth)
   xs_pool* pool = nullptr;     // engines; nullptr -> the process-wide pool
   std::mutex rand_mu;
 };

@@ -322,7 +322,7 @@ struct xs_engine {
   std::vector<CSlot> cslots;
   uint64_t c_cap_blocks = 0, c_cap_bytes = 0;
   uint64_t st_batches = 0, st_reqs = 0, st_blocks = 0;
-  std::atomic<uint64_t> st_host_md5_objs{0}, st_host_md5_bytes{0};
+  std::atomic<uint64_t> st_host_md5_objs{0}, st_host_md5_bytes{0}, st_md5_objs{0};
   // grow-only buffers of xs_engine_seal_md5 (whole objects per group)
   struct HashBufs {
     uint8_t* d_plain = nullptr;
@@ -1206,6 +1206,7 @@ static int seal_md5_impl(xs_engine* e, const uint8_t key[32], uint64_t nobj, con
   if (host_routed) *host_routed = host.count;
   e->st_host_md5_objs += host.count;
   e->st_host_md5_bytes += host.bytes;
+  e->st_md5_objs += nobj;
   return XS_OK;
 }
 
@@ -1244,10 +1245,11 @@ extern "C" void xs_engine_set_host_md5(xs_engine* e, int threads) {
   if (e) e->host_md5_threads = threads;
 }
 
-extern "C" void xs_engine_md5_stats(xs_engine* e, uint64_t out[2]) {
+extern "C" void xs_engine_md5_stats(xs_engine* e, uint64_t out[3]) {
   if (!e || !out) return;
   out[0] = e->st_host_md5_objs.load();
   out[1] = e->st_host_md5_bytes.load();
+  out[2] = e->st_md5_objs.load();
 }
 
 // ---------------------------------------------------------------- multi-device engine pool

@@ -351,6 +351,33 @@ static void test_reader_errors(rc_cipher* c, const uint8_t key[32]) {
   }
 }
 
+// read-ahead (cipher.go:726-741): one block before the first data byte; then doubling, or full
+// batches at once from a fast (memory) source under the default adaptive growth
+static void test_readahead(rc_cipher* c) {
+  const std::vector<uint8_t> plain = rbytes(40 * 65536);
+  const std::vector<uint8_t> nonce = rbytes(24);
+  for (uint32_t growth : {2u, 0u}) {
+    rc_cipher_set_batch_blocks(c, 16);
+    rc_cipher_set_readahead_growth(c, growth);
+    Src s;
+    s.p = plain.data();
+    s.n = plain.size();
+    int32_t err = 0;
+    rc_encrypter* e = rc_encrypt_data(c, mk(&s), nonce.data(), &err);
+    std::vector<uint8_t> buf(65536 + 64);
+    rc_encrypter_read(e, buf.data(), 32, &err);
+    CHECK(s.reads == 0, "reads before the header is consumed: %d", s.reads);
+    rc_encrypter_read(e, buf.data(), 1, &err);
+    CHECK(s.pos == 65536, "first data byte read %zu source bytes", s.pos);
+    rc_encrypter_read(e, buf.data(), 65535 + 16, &err);
+    rc_encrypter_read(e, buf.data(), 1, &err);
+    CHECK(s.pos == (growth == 2 ? 3u : 17u) * 65536, "growth %u: second refill ends at %zu", growth, s.pos);
+    rc_encrypter_free(e);
+  }
+  rc_cipher_set_batch_blocks(c, 64);
+  rc_cipher_set_readahead_growth(c, 0);
+}
+
 struct OpenCtx {
   const std::vector<uint8_t>* f;
   std::vector<Src*> srcs;
@@ -602,6 +629,7 @@ int main(int argc, char** argv) {
     test_concurrency(c, key);
   } else {
     test_concurrency(c, key);  // first: the decode tables are still unbuilt
+    test_readahead(c);
     test_round_trips(c, key);
     test_damaged(c, key);
     test_reader_errors(c, key);

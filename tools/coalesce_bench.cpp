@@ -2,7 +2,8 @@
 // (rc_encrypt_data + rc_decrypt_data from memory readers), T threads sharing one cipher --
 // rclone's --transfers pattern.  Run with XS_ENGINE_COALESCE=0/1 to compare one GPU round trip
 // per handle batch against cross-handle coalescing.  Verifies every round trip.
-// usage: coalesce_bench <threads> <objects_per_thread> <object_bytes>
+// usage: coalesce_bench <threads> <objects_per_thread> <object_bytes> [readahead_first_blocks]
+//        (readahead 1 = default adaptive read-ahead; 0 = full batch_blocks from the first refill)
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -34,6 +35,7 @@ int main(int argc, char** argv) {
   rc_cipher* c = rc_cipher_new("potato", "", &e);
   if (!c) return 1;
   rc_cipher_set_batch_blocks(c, 64);
+  if (argc > 4) rc_cipher_set_readahead(c, (uint32_t)atoi(argv[4]));
   std::vector<uint8_t> src((size_t)S);
   for (int64_t i = 0; i < S; i++) src[(size_t)i] = (uint8_t)(i * 7 + 3);
   // warm the engine
@@ -88,8 +90,9 @@ int main(int argc, char** argv) {
   const double gib = 2.0 * T * K * (double)S / (1 << 30);  // encrypt + decrypt
   const char* co = getenv("XS_ENGINE_COALESCE");
   printf("{\"threads\": %d, \"objects\": %d, \"object_bytes\": %lld, \"coalesce\": %s, \"seconds\": %.4f, "
-         "\"GiB_s\": %.3f, \"objects_s\": %.0f, \"bad\": %d}\n",
-         T, T * K, (long long)S, (co && atoi(co) == 0) ? "false" : "true", el, gib / el, 2.0 * T * K / el, bad.load());
+         "\"GiB_s\": %.3f, \"objects_s\": %.0f, \"readahead\": %d, \"bad\": %d}\n",
+         T, T * K, (long long)S, (co && atoi(co) == 0) ? "false" : "true", el, gib / el, 2.0 * T * K / el,
+         argc > 4 ? atoi(argv[4]) : 1, bad.load());
   rc_cipher_free(c);
   return bad.load() != 0;
 }
