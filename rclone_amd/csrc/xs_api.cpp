@@ -332,6 +332,8 @@ struct xs_engine {
     uint8_t* d_digest = nullptr;
     BlockKey* d_keys = nullptr;
     size_t plain_cap = 0, body_cap = 0, desc_cap = 0, mdesc_cap = 0, digest_cap = 0, keys_cap = 0;
+    uint8_t* route[2] = {nullptr, nullptr};  // pinned: host-routed bodies of seal_md5 groups
+    size_t route_cap[2] = {0, 0};
     hipStream_t aux = nullptr;        // wire-body D2H, overlapped with the MD5 lanes
     hipEvent_t ev_sealed = nullptr;   // the group's seal is done (aux may copy the bodies)
   } hb;
@@ -367,6 +369,17 @@ static bool grow(uint8_t** p, size_t* cap, size_t need) {
   *cap = 0;
   if (hipMalloc(p, need ? need : 16) != hipSuccess) return false;
   *cap = need;
+  return true;
+}
+
+static bool grow_pinned(uint8_t** p, size_t* cap, size_t need) {  // grow-only (x1.5), contents dropped
+  if (*cap >= need) return true;
+  (void)hipHostFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  const size_t want = std::max(need, need / 2 * 3);
+  if (hipHostMalloc((void**)p, want ? want : 16, hipHostMallocPortable) != hipSuccess) return false;
+  *cap = want;
   return true;
 }
 
@@ -408,6 +421,7 @@ static void engine_free(xs_engine* e) {
     (void)hipStreamDestroy(e->hb.aux);
   }
   if (e->hb.ev_sealed) (void)hipEventDestroy(e->hb.ev_sealed);
+  for (auto* r : e->hb.route) (void)hipHostFree(r);
   delete e;
 }
 
@@ -966,7 +980,11 @@ static int host_md5_threads_default() {
   return (int)std::max(1u, std::min(8u, hc ? hc / 2 : 1u));
 }
 
-constexpr uint64_t kHostMd5Min = 1ull << 20;  // below this an object stays on its GPU lane
+// Below this an object stays on its GPU lane: a 16 MiB lane takes ~0.24 s, longer than a 4 GiB
+// group's PCIe copies; shorter objects finish within the group's own copy time, and hashing them on
+// host cores only competes with the file reads feeding the next group (configs[4]'s 4 KiB-8 MiB
+// tree measured no gain, profiles/r02/e2e_routing_ab.jsonl).
+constexpr uint64_t kHostMd5Min = 16ull << 20;
 
 // Which objects of a group go to the host (route[k] = 1): take the longest first while the host
 // pool's makespan stays below that object's GPU lane time, i.e. while moving it shortens the
@@ -999,21 +1017,23 @@ struct HostMd5Pool {
     const uint8_t* body;
     uint64_t len;
     uint8_t* out;
-    std::unique_ptr<uint8_t[]> own;  // body copy when the caller gets no wire bodies back
+    int tag;  // staging buffer the body sits in (-1: the caller's body buffer)
   };
   std::mutex mu;
-  std::condition_variable cv;
+  std::condition_variable cv, idle;
   std::vector<Job> jobs;
   size_t next = 0;
   bool closing = false;
   std::vector<std::thread> th;
   uint64_t bytes = 0, count = 0;
+  int pending[2] = {0, 0};  // unfinished jobs per staging buffer
 
-  void push(Job&& j, int max_threads) {
+  void push(const Job& j, int max_threads) {
     std::lock_guard<std::mutex> g(mu);
     bytes += j.len;
     count++;
-    jobs.push_back(std::move(j));
+    if (j.tag >= 0) pending[j.tag]++;
+    jobs.push_back(j);
     if ((int)th.size() < max_threads && th.size() < jobs.size() - next) th.emplace_back([this] { work(); });
     cv.notify_one();
   }
@@ -1022,21 +1042,20 @@ struct HostMd5Pool {
     for (;;) {
       cv.wait(lk, [&] { return next < jobs.size() || closing; });
       if (next >= jobs.size()) return;
-      Job& j = jobs[next++];  // jobs only grow; index stays valid, element moves on realloc
-      uint8_t prefix[32];
-      memcpy(prefix, j.prefix, 32);
-      const uint8_t* body = j.own ? j.own.get() : j.body;
-      const uint64_t len = j.len;
-      uint8_t* out = j.out;
-      std::unique_ptr<uint8_t[]> own = std::move(j.own);
+      const Job j = jobs[next++];
       lk.unlock();
       HostMd5 m;
-      m.update(prefix, 32);
-      m.update(body, len);
-      m.final(out);
-      own.reset();
+      m.update(j.prefix, 32);
+      m.update(j.body, j.len);
+      m.final(j.out);
       lk.lock();
+      if (j.tag >= 0 && --pending[j.tag] == 0) idle.notify_all();
     }
+  }
+  // every job reading staging buffer `tag` is done (it may be overwritten)
+  void wait_tag(int tag) {
+    std::unique_lock<std::mutex> lk(mu);
+    idle.wait(lk, [&] { return pending[tag] == 0; });
   }
   void finish() {
     {
@@ -1084,7 +1103,7 @@ static int seal_md5_impl(xs_engine* e, const uint8_t key[32], uint64_t nobj, con
   std::vector<uint64_t> wlen, gpu_obj, host_obj;
   std::vector<uint8_t> route, dig;
   uint64_t o0 = 0, body_pos = 0;
-  while (o0 < nobj) {
+  for (uint64_t group = 0; o0 < nobj; group++) {
     uint64_t o1 = o0, lo = UINT64_MAX, hi = 0, bsum = 0, nblk = 0;
     while (o1 < nobj) {
       const uint64_t nlo = std::min(lo, offs[o1]), nhi = std::max(hi, offs[o1] + lens[o1]);
@@ -1160,18 +1179,26 @@ static int seal_md5_impl(xs_engine* e, const uint8_t key[32], uint64_t nobj, con
     hipStream_t ax = hb.aux;
     if (err == hipSuccess) err = hipEventRecord(hb.ev_sealed, st);
     if (err == hipSuccess) err = hipStreamWaitEvent(ax, hb.ev_sealed, 0);
-    std::vector<std::unique_ptr<uint8_t[]>> own(host_obj.size());
-    if (!body) {
+    // without caller bodies (cryptcheck) the routed bodies land in one of two pinned staging
+    // buffers, alternating by group, so the host can still be hashing group g while g+1 lands
+    const int tag = (int)(group & 1);
+    std::vector<uint64_t> spos(host_obj.size());
+    if (!body && !host_obj.empty()) {
+      uint64_t need = 0;
+      for (size_t k = 0; k < host_obj.size(); k++) {
+        spos[k] = need;
+        need += wlen[host_obj[k] - o0];
+      }
+      host.wait_tag(tag);
+      if (!grow_pinned(&hb.route[tag], &hb.route_cap[tag], need)) {
+        set_error("xs_engine_seal_md5: pinned staging of %llu bytes failed", (unsigned long long)need);
+        return XS_ERR_NOMEM;
+      }
       for (size_t k = 0; k < host_obj.size() && err == hipSuccess; k++) {
         const uint64_t i = host_obj[k], len = wlen[i - o0];
-        own[k].reset(new (std::nothrow) uint8_t[len ? len : 1]);
-        if (!own[k]) {
-          set_error("xs_engine_seal_md5: host allocation of %llu bytes failed", (unsigned long long)len);
-          return XS_ERR_NOMEM;
-        }
-        if (len) err = hipMemcpyAsync(own[k].get(), hb.d_body + wpos[i - o0], len, hipMemcpyDeviceToHost, ax);
+        if (len) err = hipMemcpyAsync(hb.route[tag] + spos[k], hb.d_body + wpos[i - o0], len, hipMemcpyDeviceToHost, ax);
       }
-    } else if (w && err == hipSuccess) {
+    } else if (body && w && err == hipSuccess) {
       err = hipMemcpyAsync(body + body_pos, hb.d_body, w, hipMemcpyDeviceToHost, ax);
     }
     if (err != hipSuccess) return hip_fail(err, "D2H");
@@ -1189,11 +1216,11 @@ static int seal_md5_impl(xs_engine* e, const uint8_t key[32], uint64_t nobj, con
       HostMd5Pool::Job j;
       memcpy(j.prefix, magic, 8);
       memcpy(j.prefix + 8, nonces + 24 * i, 24);
-      j.body = body ? body + body_pos + wpos[i - o0] : nullptr;
+      j.body = body ? body + body_pos + wpos[i - o0] : hb.route[tag] + spos[k];
       j.len = wlen[i - o0];
       j.out = md5 + 16 * i;
-      j.own = std::move(own[k]);
-      host.push(std::move(j), host_threads);
+      j.tag = body ? -1 : tag;
+      host.push(j, host_threads);
     }
     // the host-side descriptor vectors are reused next group: wait for this group's copies
     err = hipStreamSynchronize(st);

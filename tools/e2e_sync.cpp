@@ -23,8 +23,15 @@
 //   verify : sampled objects decrypted back through rc_decrypt_data (GPU) and compared with the
 //            local bytes; one stored object corrupted -> cryptcheck must flag exactly that one.
 // Prints one JSON line.
+//   anchor : with --anchor FILE, one JSON line per sampled object (the edge files, ~64 spread
+//            over the tree, the largest): plaintext seed and size, nonce, SHA-256 of the stored
+//            crypt file (header || wire body as the memory remote holds it) and the tee MD5 --
+//            tests/test_e2e_anchor_gpu.py recomputes them with the CPU oracle.
+//   devices: --devices 0,1,... puts lane l's engine on device list[l % n] and the rc_* handles
+//            and name engines on the same list (RCLONE_AMD_DEVICES): one process over several GPUs.
 //   usage: e2e_sync [--gib G] [--dir D] [--transfers T] [--mode batch|stream]
 //                   [--check-dst-hash 0|1] [--group-mib M] [--lanes L] [--keep]
+//                   [--anchor FILE] [--devices LIST]
 #include <fcntl.h>
 #include <sys/random.h>
 #include <sys/stat.h>
@@ -106,6 +113,75 @@ struct Md5 {
     memcpy(out, h, 16);
   }
 };
+
+// ---------------------------------------------------------------- SHA-256 (FIPS 180-4), host
+// for --anchor: digests of sampled stored crypt files, checked by the test suite against the
+// oracle's crypt files (tests/test_e2e_anchor_gpu.py)
+struct Sha256 {
+  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au, 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  uint8_t buf[64];
+  uint64_t n = 0;
+  static uint32_t ror(uint32_t x, int c) { return (x >> c) | (x << (32 - c)); }
+  void block(const uint8_t* p) {
+    static const uint32_t K[64] = {
+        0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+        0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+        0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+        0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+        0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+        0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+        0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+        0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+    uint32_t w[64];
+    for (int i = 0; i < 16; i++) w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+    for (int i = 16; i < 64; i++) {
+      const uint32_t s0 = ror(w[i - 15], 7) ^ ror(w[i - 15], 18) ^ (w[i - 15] >> 3);
+      const uint32_t s1 = ror(w[i - 2], 17) ^ ror(w[i - 2], 19) ^ (w[i - 2] >> 10);
+      w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+    }
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+    for (int i = 0; i < 64; i++) {
+      const uint32_t t1 = hh + (ror(e, 6) ^ ror(e, 11) ^ ror(e, 25)) + ((e & f) ^ (~e & g)) + K[i] + w[i];
+      const uint32_t t2 = (ror(a, 2) ^ ror(a, 13) ^ ror(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+  }
+  void update(const uint8_t* p, size_t len) {
+    size_t have = n & 63;
+    n += len;
+    if (have) {
+      const size_t k = std::min(len, 64 - have);
+      memcpy(buf + have, p, k);
+      p += k;
+      len -= k;
+      if (have + k < 64) return;
+      block(buf);
+    }
+    for (; len >= 64; p += 64, len -= 64) block(p);
+    memcpy(buf, p, len);
+  }
+  void final(uint8_t out[32]) {
+    const uint64_t bits = n * 8;
+    const uint8_t one = 0x80, zero = 0;
+    update(&one, 1);
+    while ((n & 63) != 56) update(&zero, 1);
+    uint8_t lb[8];
+    for (int i = 0; i < 8; i++) lb[i] = (uint8_t)(bits >> (56 - 8 * i));
+    update(lb, 8);
+    for (int i = 0; i < 8; i++)
+      for (int k = 0; k < 4; k++) out[4 * i + k] = (uint8_t)(h[i] >> (24 - 8 * k));
+  }
+};
+static std::string hexs(const uint8_t* p, size_t n) {
+  static const char* d = "0123456789abcdef";
+  std::string s;
+  for (size_t i = 0; i < n; i++) {
+    s += d[p[i] >> 4];
+    s += d[p[i] & 15];
+  }
+  return s;
+}
 
 // ---------------------------------------------------------------- helpers
 static double now() {
@@ -236,6 +312,7 @@ int main(int argc, char** argv) {
   std::string dir = "/tmp/rc_e2e_src", mode = "batch";
   int transfers = 16, check_dst = 1, keep = 0, nlanes = 4;
   uint64_t group_mib = 4096;
+  std::string anchor, devices;
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
     auto nx = [&] { return std::string(i + 1 < argc ? argv[++i] : ""); };
@@ -247,12 +324,27 @@ int main(int argc, char** argv) {
     else if (a == "--group-mib") group_mib = strtoull(nx().c_str(), nullptr, 10);
     else if (a == "--keep") keep = 1;
     else if (a == "--lanes") nlanes = std::max(1, atoi(nx().c_str()));
+    else if (a == "--anchor") anchor = nx();
+    else if (a == "--devices") devices = nx();
     else {
       fprintf(stderr, "unknown argument %s\n", a.c_str());
       return 2;
     }
   }
   if (mode != "batch" && mode != "stream") return 2;
+  std::vector<int> devs;
+  if (!devices.empty()) {
+    setenv("RCLONE_AMD_DEVICES", devices.c_str(), 1);  // rc_* handles and name engines
+    for (const char* p = devices.c_str(); *p;) {
+      char* end = nullptr;
+      const long d = strtol(p, &end, 10);
+      if (end == p) break;
+      devs.push_back((int)d);
+      p = end;
+      while (*p == ',') p++;
+    }
+  }
+  if (devs.empty()) devs.push_back(0);
   // ---- local tree
   std::vector<Obj> objs;
   {
@@ -348,7 +440,7 @@ int main(int argc, char** argv) {
   std::vector<xs_engine*> eng(lanes);
   std::vector<uint8_t*> stage(lanes);
   for (int l = 0; l < lanes; l++) {
-    eng[l] = xs_engine_create(0, 256, 1);
+    eng[l] = xs_engine_create(devs[l % devs.size()], 256, 1);
     stage[l] = (uint8_t*)xs_host_alloc(max_group ? max_group : 16);
     if (!eng[l] || !stage[l]) {
       fprintf(stderr, "engine/staging: %s\n", xs_last_error());
@@ -516,6 +608,36 @@ int main(int argc, char** argv) {
     if (n != o.size || memcmp(got.data(), want.data(), o.size) || (e != RC_EOF && e != RC_NIL)) verify_bad++;
     verified++;
   }
+  uint64_t anchored = 0;
+  if (!anchor.empty()) {  // before the corruption below: the objects as sync stored them
+    std::vector<size_t> pick = {0, 1, 2, 3};
+    for (size_t i = 4; i < objs.size(); i += std::max<size_t>(1, objs.size() / 64)) pick.push_back(i);
+    size_t largest = 0;
+    for (size_t i = 0; i < objs.size(); i++)
+      if (objs[i].size > objs[largest].size) largest = i;
+    pick.push_back(largest);
+    pick.push_back(objs.size() - 1);
+    std::sort(pick.begin(), pick.end());
+    pick.erase(std::unique(pick.begin(), pick.end()), pick.end());
+    FILE* f = fopen(anchor.c_str(), "w");
+    if (!f) {
+      failures++;
+    } else {
+      for (size_t i : pick) {
+        const Obj& o = objs[i];
+        Sha256 h;
+        h.update(o.header, 32);
+        h.update(o.body, o.body_len);
+        uint8_t d[32];
+        h.final(d);
+        fprintf(f, "{\"index\": %zu, \"size\": %llu, \"seed\": %llu, \"nonce\": \"%s\", \"sha256\": \"%s\", "
+                "\"tee_md5\": \"%s\"}\n", i, (unsigned long long)o.size, (unsigned long long)(0xF11E0000ull + i),
+                hexs(o.header + 8, 24).c_str(), hexs(d, 32).c_str(), hexs(o.tee, 16).c_str());
+        anchored++;
+      }
+      fclose(f);
+    }
+  }
   // corruption: flip one ciphertext byte of one stored object, drop its cached hash
   size_t victim = objs.size() / 2;
   while (victim < objs.size() && objs[victim].body_len < 100) victim++;
@@ -538,13 +660,13 @@ int main(int argc, char** argv) {
          "\"cryptcheck_differences\": %llu, \"verified_objects\": %llu, \"verify_failures\": %llu, "
          "\"corruption_flagged\": %llu, \"names_encrypt_s\": %.4f, \"names_decrypt_s\": %.4f, "
          "\"name_mismatches\": %llu, \"example_remote_name\": \"%s\", "
-         "\"tree_write_s\": %.2f, \"lane_seconds\": {\"sync_read\": %.3f, "
+         "\"anchored_objects\": %llu, \"devices\": \"%s\", \"tree_write_s\": %.2f, \"lane_seconds\": {\"sync_read\": %.3f, "
          "\"sync_gpu\": %.3f, \"check_read\": %.3f, \"check_gpu\": %.3f}, \"ok\": %s}\n",
          mode.c_str(), objs.size(), g, transfers, lanes, (unsigned long long)group_mib, t_sync, g / t_sync, t_dst,
          check_dst ? g / (t_sync + t_dst) : 0.0, t_check, g / t_check, (unsigned long long)put_mismatch,
          (unsigned long long)ndiff, (unsigned long long)verified, (unsigned long long)verify_bad,
          (unsigned long long)flagged, t_names_enc, t_names_dec, (unsigned long long)name_mismatch,
-         objs.empty() ? "" : objs.back().remote.c_str(), t_gen, sync_read, sync_gpu, check_read, check_gpu, ok ? "true" : "false");
+         objs.empty() ? "" : objs.back().remote.c_str(), (unsigned long long)anchored, devices.c_str(), t_gen, sync_read, sync_gpu, check_read, check_gpu, ok ? "true" : "false");
   for (int l = 0; l < lanes; l++) {
     xs_engine_destroy(eng[l]);
     xs_host_free(stage[l]);

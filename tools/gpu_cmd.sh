@@ -1,10 +1,13 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_readahead_gpu.py tests/test_cipher_gpu.py > gpurun_out/r02d.tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/r02d.tests.log; exit 1; }
-tail -3 gpurun_out/r02d.tests.log
-rm -f gpurun_out/r02d.coalesce.jsonl
-for rep in 1 2 3; do for S in 65536 1048576 8388608; do for ra in 1 0; do
-  K=$((800*65536/S)); [ $K -lt 16 ] && K=16
-  timeout -k 10 120 ./tools/coalesce_bench 16 $K $S $ra >> gpurun_out/r02d.coalesce.jsonl || exit 1
-done; done; done
-cat gpurun_out/r02d.coalesce.jsonl
+rm -f gpurun_out/r02g.e2e.jsonl
+for ht in 0 8 0 8; do
+  XS_MD5_HOST_THREADS=$ht timeout -k 10 300 ./tools/e2e_sync --gib 32 --dir /dev/shm/rc_e2e_ab --lanes 4 --transfers 16 >> gpurun_out/r02g.e2e.jsonl 2>>gpurun_out/r02g.e2e.err || { echo E2E_FAILED; tail gpurun_out/r02g.e2e.err; rm -rf /dev/shm/rc_e2e_ab; exit 1; }
+  echo "host_threads=$ht done"
+done
+rm -rf /dev/shm/rc_e2e_ab
+python3 -c "
+import json
+for l in open('gpurun_out/r02g.e2e.jsonl'):
+    d=json.loads(l); print(d['sync_GiB_s'], d['cryptcheck_GiB_s'], d['lane_seconds'], d['ok'])
+"
