@@ -43,7 +43,10 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=10, help="untimed steps; the clock settles over the first ~6")
+    ap.add_argument("--warmup", type=int, default=10, help="untimed steps (at least --warmup-seconds of them)")
+    ap.add_argument("--warmup-seconds", type=float, default=2.0,
+                    help="minimum back-to-back warm-up time: the DVFS clock settles after >= 2 s of load "
+                         "(MI355X_MICROARCH.md)")
     ap.add_argument("--blocks", type=int, default=100_000, help="64 KiB blocks per GPU")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -95,42 +98,69 @@ def cpu_baseline(seconds):
 
 
 def load_traffic():
-    """HBM bytes per xs_crypt launch from the committed rocprofv3 PMC summary (or None)."""
+    """HBM bytes and VALU instructions per xs_crypt launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, tools/make_traffic.py), or ({}, reason) when there is none or it
+    was measured on other kernel sources than the ones built here (sha256 stamp)."""
+    from rclone_amd.build import kernel_sources_sha256
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
-        return None
+        return {}, "no profiles/pmc_traffic.json"
     try:
         with open(p) as f:
             d = json.load(f)
-        return d
-    except Exception:
-        return None
+    except Exception as exc:  # noqa: BLE001
+        return {}, f"unreadable pmc_traffic.json: {exc}"
+    have = kernel_sources_sha256()
+    if d.get("kernel_sources_sha256") != have:
+        return {}, (f"stale: counters measured on kernel sources {d.get('kernel_sources_sha256', 'unstamped')[:12]}, "
+                    f"tree has {have[:12]}")
+    return d, None
 
 
-def sustained_clock():
-    """Shader clock measured under this kernel's own load (profiles/clock_probe.json)."""
-    p = os.path.join(ROOT, "profiles", "clock_probe.json")
-    try:
-        with open(p) as f:
-            return float(json.load(f)["sustained_shader_clock_ghz"]) * 1e9
-    except Exception:
-        return None
+class ClockProbe:
+    """In-window shader clock: one wave beside the crypt kernels (xs_clock_probe_dev, own stream)
+    compares s_memtime with the 100 MHz s_memrealtime.  It is launched as the timed region opens
+    and ends by itself after a set share of the expected window, so the closing device
+    synchronize never waits for it."""
+
+    def __init__(self, L, dev):
+        import torch
+        self.L, self.torch = L, torch
+        self.stop = torch.zeros(1, dtype=torch.int32, device=dev)  # never raised: the probe ends by time
+        self.out = torch.zeros(5, dtype=torch.int64, device=dev)
+        self.stream = torch.cuda.Stream(dev)
+
+    def start(self, seconds):
+        import ctypes as ct
+        from rclone_amd import _lib
+        _lib.check(self.L.xs_clock_probe_dev(self.stop.data_ptr(), self.out.data_ptr(), max(seconds, 1e-4),
+                                             ct.c_void_p(self.stream.cuda_stream)), "clock probe")
+
+    def result(self):
+        self.stream.synchronize()
+        t0, r0, t1, r1, n = [int(x) for x in self.out.cpu().tolist()]
+        if r1 <= r0:
+            return None
+        return {"shader_clock_ghz": round((t1 - t0) / (r1 - r0) / 10.0, 4), "window_s": round((r1 - r0) / 1e8, 4),
+                "samples": n, "source": "xs_clock_probe_dev: s_memtime / s_memrealtime (100 MHz), one wave on a side "
+                                       "stream over the first 80% of the timed steps"}
 
 
-def issue_bound(valu_insts, ms):
-    """VALU issue bound of a launch: integer VALU wave-instructions x 4 cycles (measured on
-    gfx950: tools/microbench/issuebench.hip) spread over 256 CUs x 4 SIMDs, at the 2.4 GHz peak
-    clock and at the sustained clock measured under this kernel (profiles/clock_probe.json)."""
+def issue_bound(valu_insts, ms, clock_hz=None):
+    """VALU roofline of a launch: integer VALU wave-instructions (rocprofv3 SQ_INSTS_VALU) issued
+    per second against the chip's issue peak, 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64
+    integer instruction (measured on gfx950: tools/microbench/issuebench.hip) = 614.4 G
+    wave-instructions/s; and the same bound at the clock measured in the timed window."""
     if not valu_insts:
         return None
-    bound_ms = valu_insts * VALU_CYC / (SIMDS * CLOCK_HZ) * 1e3
-    res = {"valu_wave_insts": valu_insts, "cycles_per_inst": VALU_CYC, "bound_ms_2p4ghz": round(bound_ms, 4),
-           "frac_2p4ghz": round(bound_ms / ms, 4)}
-    clk = sustained_clock()
-    if clk:
-        b2 = valu_insts * VALU_CYC / (SIMDS * clk) * 1e3
-        res.update({"sustained_clock_ghz": round(clk / 1e9, 3), "bound_ms_sustained": round(b2, 4),
-                    "frac_sustained": round(b2 / ms, 4)})
+    peak = SIMDS * CLOCK_HZ / VALU_CYC / 1e9
+    achieved = valu_insts / (ms * 1e-3) / 1e9
+    res = {"bound": "valu", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "G wave-instr/s",
+           "frac": round(achieved / peak, 4), "valu_wave_insts": valu_insts, "cycles_per_inst": VALU_CYC}
+    if clock_hz:
+        peak_w = SIMDS * clock_hz / VALU_CYC / 1e9
+        res.update({"window_clock_ghz": round(clock_hz / 1e9, 4), "peak_at_window_clock": round(peak_w, 1),
+                    "frac_at_window_clock": round(achieved / peak_w, 4)})
     return res
 
 
@@ -550,9 +580,17 @@ def main():
             b.record(stream)
             ev.append((False, a, b))
 
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize(dev)
+    tw = time.perf_counter()
+    nwarm, tail = 0, []
+    while nwarm < args.warmup or time.perf_counter() - tw < args.warmup_seconds:
+        ts = time.perf_counter()
+        for _ in range(4):
+            step(False)
+        torch.cuda.synchronize(dev)  # keep the host within a few steps of the device
+        tail = (tail + [(time.perf_counter() - ts) / 4])[-4:]
+        nwarm += 4
+    warm_s = time.perf_counter() - tw
+    step_s = sorted(tail)[len(tail) // 2]  # settled per-step time: sizes the clock probe's window
     # correctness gate before timing: round trip + every tag verified + sampled blocks
     # bit-exact against the oracle (rank 0 only; the oracle is the checker, never timed)
     if not (torch.equal(out, plain) and int(ok.sum()) == nb):
@@ -566,14 +604,17 @@ def main():
                 raise SystemExit("bench: block %d differs from the oracle" % i)
     if world > 1:
         dist.barrier()
+    probe = ClockProbe(L, dev)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    probe.start(0.8 * args.steps * step_s)
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    clock = probe.result()
     # counters and max time over ranks (RCCL, small tensors only)
     from rclone_amd.objectset import tag_digest
     counters = torch.tensor([args.steps * 2 * nb, args.steps * 2 * plain_len, int(nb - int(ok.sum())), 0, 0],
@@ -596,10 +637,11 @@ def main():
     if rank == 0:
         ach_seal = ALG_BYTES_SEAL * nb / (seal_avg * 1e-3) / 1e9
         ach_open = ALG_BYTES_OPEN * nb / (open_avg * 1e-3) / 1e9
-        tr = load_traffic() or {}
+        tr, stale = load_traffic()
         # PMC figures are per launch of the default workload; scale if nb differs
         pmc_nb = tr.get("blocks_per_launch", nb)
         scale = nb / pmc_nb if pmc_nb else 1.0
+        clk_hz = clock["shader_clock_ghz"] * 1e9 if clock else None
 
         def per(key):
             v = tr.get(key)
@@ -630,12 +672,15 @@ def main():
                          "traffic": per("seal_bytes_per_launch"),
                          "kernel_ms_avg": round(seal_avg, 4),
                          "alg_bytes_per_launch": ALG_BYTES_SEAL * nb,
-                         "traffic_source": tr.get("source"),
-                         "valu_issue": issue_bound(per("seal_valu_wave_insts_per_launch"), seal_avg),
+                         "traffic_source": tr.get("source") if tr else stale,
+                         "traffic_git_head": tr.get("git_head"),
+                         "valu": issue_bound(per("seal_valu_wave_insts_per_launch"), seal_avg, clk_hz),
                          "open": {"kernel": "xs_open", "achieved": round(ach_open, 1),
                                   "frac": round(ach_open / HBM_PEAK_GBS, 4), "kernel_ms_avg": round(open_avg, 4),
                                   "traffic": per("open_bytes_per_launch"),
-                                  "valu_issue": issue_bound(per("open_valu_wave_insts_per_launch"), open_avg)}},
+                                  "valu": issue_bound(per("open_valu_wave_insts_per_launch"), open_avg, clk_hz)}},
+            "clock": clock,
+            "warmup_s": round(warm_s, 3), "warmup_steps": nwarm,
             "counters": {"blocks": int(counters[0].item()), "bytes": total_bytes,
                          "tag_failures": int(counters[2].item()),
                          "tag_digest": "%016x%016x" % (int(counters[4].item()) & (2**64 - 1),

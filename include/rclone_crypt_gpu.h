@@ -119,6 +119,12 @@ int xs_fill_random_dev(void *d, uint64_t nbytes, uint64_t seed, void *stream);
 int xs_fill_blocks_dev(void *d, uint64_t nblocks, uint64_t first_block, uint64_t block_stride, uint64_t seed,
                        void *stream);
 
+/* Shader-clock probe (benchmarking): one wave on `stream` records s_memtime against the 100 MHz
+ * s_memrealtime until *d_stop (device memory, 0 at launch) becomes non-zero or max_seconds pass;
+ * d_out[0..4] = start shader ticks, start 100 MHz ticks, end shader ticks, end 100 MHz ticks,
+ * samples.  Clock (GHz) = (d_out[2]-d_out[0]) / (d_out[3]-d_out[1]) / 10. */
+int xs_clock_probe_dev(const uint32_t *d_stop, uint64_t *d_out, double max_seconds, void *stream);
+
 /* MD5 of n streams in HBM, one lane per stream (crypt.go:516-533 put's ciphertext hash,
  * :784-806 computeHashWithNonce): d_digest[16*i] = MD5(prefix_i || src[off_i : off_i+len_i]).
  * An invalid descriptor (bounds, alignment, prefix_len) gets d_ok[i] = 0 (d_ok may be NULL)

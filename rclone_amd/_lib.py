@@ -57,6 +57,7 @@ _SIGS = [
     ("xs_fill_random_dev", ctypes.c_int, [vp, u64, u64, vp]),
     ("xs_fill_blocks_dev", ctypes.c_int, [vp, u64, u64, u64, u64, vp]),
     ("xs_md5_batch_dev", ctypes.c_int, [vp, u64, vp, u64, vp, vp, vp]),
+    ("xs_clock_probe_dev", ctypes.c_int, [vp, vp, ctypes.c_double, vp]),
     ("xs_engine_create", vp, [ctypes.c_int, ctypes.c_uint32, ctypes.c_int]),
     ("xs_engine_destroy", None, [vp]),
     ("xs_engine_seal", ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, u64, vp, u64, vp]),

@@ -14,7 +14,26 @@ LIB = os.path.join(HERE, "librclone_crypt.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RCLONE_AMD_ARCH", "gfx950")
 
-SOURCES = ["xs_kernels.hip", "xs_md5.hip", "xs_eme.hip", "xs_api.cpp", "cipher.cpp", "names.cpp", "names_gpu.cpp", "scrypt.cpp"]
+SOURCES = ["xs_kernels.hip", "xs_md5.hip", "xs_eme.hip", "xs_probe.hip", "xs_api.cpp", "cipher.cpp", "names.cpp", "names_gpu.cpp", "scrypt.cpp"]
+
+
+# what the crypt kernels (xs_seal / xs_open / keygen) are compiled from: PMC counters committed under
+# profiles/ (tools/make_traffic.py) are valid only for this exact set of bytes
+KERNEL_SOURCES = ["rclone_amd/csrc/xs_kernels.hip", "rclone_amd/csrc/xs_salsa_lazy.h", "rclone_amd/csrc/xs_salsa_asm.h",
+                  "rclone_amd/csrc/xs_internal.h"]
+
+
+def kernel_sources_sha256(root=None):
+    import hashlib
+    root = root or os.path.dirname(HERE)
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        p = os.path.join(root, rel)
+        h.update(rel.encode() + b"\0")
+        if os.path.exists(p):
+            with open(p, "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()
 
 
 def sources():

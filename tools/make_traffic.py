@@ -8,17 +8,34 @@ bytes of a wide (16 B/lane) streaming read -- global_load and LDS-DMA alike -- s
 Also records SQ_INSTS_VALU (wave-instructions) per launch for the VALU issue bound."""
 import json
 import os
+import subprocess
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import load  # noqa: E402
 
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from rclone_amd.build import KERNEL_SOURCES, kernel_sources_sha256  # noqa: E402
+
+
+def git_head(root=ROOT):
+    try:
+        return subprocess.check_output(["git", "-C", root, "rev-parse", "HEAD"], text=True).strip()
+    except Exception:  # noqa: BLE001 -- the GPU box has no .git
+        return os.environ.get("RCLONE_AMD_GIT_HEAD", "unknown")
+
+
 def main():
     d, out = sys.argv[1], sys.argv[2]
     acc = load(d)
-    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE ({d}), reads x2 (gfx950 FETCH_SIZE halving)",
-           "blocks_per_launch": int(sys.argv[3]) if len(sys.argv) > 3 else 100_000}
+    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU ({d}), one pass per counter group, "
+                     "reads x2 (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md HBM section)",
+           "blocks_per_launch": int(sys.argv[3]) if len(sys.argv) > 3 else 100_000,
+           "kernel_sources_sha256": kernel_sources_sha256(),
+           "kernel_sources": KERNEL_SOURCES,
+           "git_head": git_head()}
     for k, cs in acc.items():
         for name, key in (("xs_seal", "seal"), ("xs_open", "open")):
             if name in k and "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
