@@ -231,6 +231,9 @@ typedef struct rc_reader {
   rc_read_fn read;
   rc_close_fn close;           /* may be NULL (io.NopCloser) */
   rc_range_seek_fn range_seek; /* may be NULL */
+  /* Opaque: never dereferenced, only passed back to the callbacks.  A cgo binding stores a
+   * cgo.Handle here as (void *)(uintptr_t)h from C code and gets it back as uintptr_t
+   *  -- Go code never converts the integer to unsafe.Pointer. */
   void *user;
 } rc_reader;
 /* OpenRangeSeek (cipher.go:77): open the underlying object at (offset, limit). */
@@ -245,6 +248,9 @@ typedef struct rc_decrypter rc_decrypter;
 rc_cipher *rc_cipher_new(const char *password, const char *salt, int32_t *err);
 int32_t rc_cipher_key(rc_cipher *c, const char *password, const char *salt);
 void rc_cipher_keys(const rc_cipher *c, uint8_t data_key[32], uint8_t name_key[32], uint8_t name_tweak[16]);
+/* Install keys derived elsewhere (a Go binding that already ran Cipher.Key, cipher.go:231). */
+void rc_cipher_set_keys(rc_cipher *c, const uint8_t data_key[32], const uint8_t name_key[32],
+                        const uint8_t name_tweak[16]);
 void rc_cipher_set_pass_bad_blocks(rc_cipher *c, int32_t pass); /* setPassBadBlocks :217 */
 void rc_cipher_set_rand(rc_cipher *c, rc_reader rand);           /* c.cryptoRand */
 /* Read-ahead of encrypters/decrypters.  The first refill of a stream, and the first after a

@@ -82,6 +82,7 @@ _SIGS = [
     ("rc_cipher_new", vp, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(i32)]),
     ("rc_cipher_key", i32, [vp, ctypes.c_char_p, ctypes.c_char_p]),
     ("rc_cipher_keys", None, [vp, vp, vp, vp]),
+    ("rc_cipher_set_keys", None, [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]),
     ("rc_cipher_set_pass_bad_blocks", None, [vp, i32]),
     ("rc_cipher_set_rand", None, [vp, RcReader]),
     ("rc_cipher_set_batch_blocks", None, [vp, ctypes.c_uint32]),

@@ -197,6 +197,14 @@ extern "C" rc_cipher* rc_cipher_new(const char* password, const char* salt, int3
   return c;
 }
 
+extern "C" void rc_cipher_set_keys(rc_cipher* c, const uint8_t data_key[32], const uint8_t name_key[32],
+                                   const uint8_t name_tweak[16]) {
+  memcpy(c->data_key, data_key, 32);
+  memcpy(c->name_key, name_key, 32);
+  memcpy(c->name_tweak, name_tweak, 16);
+  xs::aes::expand_key(c->name_key, c->name_tweak, &c->eme);
+}
+
 extern "C" void rc_cipher_keys(const rc_cipher* c, uint8_t data_key[32], uint8_t name_key[32], uint8_t name_tweak[16]) {
   if (data_key) memcpy(data_key, c->data_key, 32);
   if (name_key) memcpy(name_key, c->name_key, 32);

@@ -1,8 +1,10 @@
-/* TEST INFRASTRUCTURE: a C11 client of librclone_crypt.so shaped exactly like the cgo binding in
- * INTEGRATION.md.  Go keeps each io.Reader / opener behind a cgo.Handle -- a small integer -- and
- * passes it through the C ABI's opaque `user` pointer as (void *)(uintptr_t)h; the Go callbacks
- * (goRead / goClose / goOpen below) receive it back as uintptr_t, never as a pointer.  The checks
- * use only entry points that need no GPU (the header, error and nonce paths of cipher.go,
+/* TEST INFRASTRUCTURE: a C11 client of librclone_crypt.so through the C half of the cgo binding,
+ * integration/gpucipher/shim.c, compiled exactly as cgo would (-std=c11, the package's include
+ * path, a stand-in _cgo_export.h).  The "Go side" -- goRead / goClose / goRangeSeek / goOpen, the
+ * //export functions of gpucipher.go -- is played here by C functions that behave like them: a
+ * handle table of small integers (runtime/cgo.Handle values 1, 2, ...), never pointers, and
+ * reader / opener errors returned as codes >= RC_USER_BASE that must come back unchanged.  The
+ * checks use only entry points that need no GPU (the header, error and nonce paths of cipher.go,
  * DecryptDataSeek's open callback, sizes, nonce arithmetic, the key derivation, host-only name
  * modes), so this runs in the CPU suite; tests/test_native_sanitize.py runs it.
  * Reference: librclone/librclone.go:22-104 (the reference's cgo precedent), backend/crypt/cipher.go. */
@@ -10,7 +12,14 @@
 #include <stdio.h>
 #include <string.h>
 
-#include "../../include/rclone_crypt_gpu.h"
+#include "_cgo_export.h"
+#include "rclone_crypt_gpu.h"
+
+/* shim.c */
+rc_reader gpucipher_reader(uintptr_t h, int closer, int range_seeker);
+rc_encrypter *gpucipher_encrypt(rc_cipher *c, uintptr_t in, const uint8_t *nonce, int32_t *err);
+rc_decrypter *gpucipher_decrypt(rc_cipher *c, uintptr_t rc, int range_seeker, int32_t *err);
+rc_decrypter *gpucipher_decrypt_seek(rc_cipher *c, uintptr_t open_state, int64_t offset, int64_t limit, int32_t *err);
 
 static int failures = 0;
 #define CHECK(c, msg)                          \
@@ -30,7 +39,7 @@ typedef struct {
 } box;
 static box boxes[8];
 
-static int64_t goRead(uintptr_t h, uint8_t *p, int64_t n, int32_t *err) {
+int64_t goRead(uintptr_t h, uint8_t *p, int64_t n, int32_t *err) {
   box *b = &boxes[h];
   b->reads++;
   int64_t k = b->n - b->pos;
@@ -40,13 +49,19 @@ static int64_t goRead(uintptr_t h, uint8_t *p, int64_t n, int32_t *err) {
   *err = (k == 0) ? b->fail : RC_NIL;
   return k;
 }
-static int32_t goClose(uintptr_t h) {
+int32_t goClose(uintptr_t h) {
   boxes[h].closes++;
+  return RC_NIL;
+}
+int32_t goRangeSeek(uintptr_t h, int64_t offset, int32_t whence, int64_t limit) {
+  (void)whence;
+  (void)limit;
+  boxes[h].pos = offset;
   return RC_NIL;
 }
 static int64_t open_calls[4][2];
 static int nopen = 0;
-static int32_t goOpen(uintptr_t h, int64_t off, int64_t lim, rc_reader *out) {
+int32_t goOpen(uintptr_t h, int64_t off, int64_t lim, rc_reader *out) {
   (void)out;
   if (nopen < 4) {
     open_calls[nopen][0] = off;
@@ -54,15 +69,6 @@ static int32_t goOpen(uintptr_t h, int64_t off, int64_t lim, rc_reader *out) {
   }
   nopen++;
   return (int32_t)(RC_USER_BASE + h); /* the opener fails with a Go error (code >= RC_USER_BASE) */
-}
-
-/* ---- the C shims of the cgo preamble: user carries the handle value */
-static int64_t cRead(void *user, uint8_t *p, int64_t n, int32_t *err) { return goRead((uintptr_t)user, p, n, err); }
-static int32_t cClose(void *user) { return goClose((uintptr_t)user); }
-static int32_t cOpen(void *user, int64_t off, int64_t lim, rc_reader *out) { return goOpen((uintptr_t)user, off, lim, out); }
-static rc_reader mkReader(uintptr_t h, int closer) {
-  rc_reader r = {cRead, closer ? cClose : 0, 0, (void *)h};
-  return r;
 }
 
 static void hex(const char *name, const uint8_t *p, int n) {
@@ -107,20 +113,20 @@ int main(void) {
   /* newDecrypter errors close the source once; a reader error passes through unchanged */
   static const uint8_t bad_magic[40] = "RCLONX\0\0--------------------------------";
   boxes[1] = (box){bad_magic, 40, 0, RC_EOF, 0, 0};
-  rc_decrypter *d = rc_decrypt_data(c, mkReader(1, 1), &err);
+  rc_decrypter *d = gpucipher_decrypt(c, 1, 0, &err);
   CHECK(!d && err == RC_ERR_BAD_MAGIC && boxes[1].closes == 1, "bad magic");
   boxes[2] = (box){bad_magic, 10, 0, RC_EOF, 0, 0};
-  d = rc_decrypt_data(c, mkReader(2, 1), &err);
+  d = gpucipher_decrypt(c, 2, 0, &err);
   CHECK(!d && err == RC_ERR_FILE_TOO_SHORT && boxes[2].closes == 1, "too short");
   boxes[3] = (box){bad_magic, 5, 0, RC_USER_BASE + 7, 0, 0};
-  d = rc_decrypt_data(c, mkReader(3, 1), &err);
+  d = gpucipher_decrypt(c, 3, 1, &err);
   CHECK(!d && err == RC_USER_BASE + 7 && boxes[3].closes == 1, "reader error passes through");
   printf("decrypter_errors %d %d %d\n", RC_ERR_BAD_MAGIC, RC_ERR_FILE_TOO_SHORT, RC_USER_BASE + 7);
 
   /* DecryptDataSeek: the opener's error passes through; open arguments as cipher.go:821-859 */
-  d = rc_decrypt_data_seek(c, cOpen, (void *)(uintptr_t)4, 0, -1, &err);
+  d = gpucipher_decrypt_seek(c, 4, 0, -1, &err);
   CHECK(!d && err == RC_USER_BASE + 4, "open error (offset 0)");
-  d = rc_decrypt_data_seek(c, cOpen, (void *)(uintptr_t)5, 100, 50, &err);
+  d = gpucipher_decrypt_seek(c, 5, 100, 50, &err);
   CHECK(!d && err == RC_USER_BASE + 5, "open error (offset 100)");
   CHECK(nopen == 2 && open_calls[0][0] == 0 && open_calls[0][1] == -1 && open_calls[1][0] == 0 &&
             open_calls[1][1] == 32,
@@ -129,9 +135,9 @@ int main(void) {
   /* encrypter: nonce from the cipher's random source, header served before any block */
   static const uint8_t rnd[24] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
   boxes[6] = (box){rnd, 24, 0, RC_EOF, 0, 0};
-  rc_cipher_set_rand(c, mkReader(6, 0));
+  rc_cipher_set_rand(c, gpucipher_reader(6, 0, 0));
   boxes[7] = (box){rnd, 0, 0, RC_EOF, 0, 0};
-  rc_encrypter *e = rc_encrypt_data(c, mkReader(7, 0), NULL, &err);
+  rc_encrypter *e = gpucipher_encrypt(c, 7, NULL, &err);
   CHECK(e && err == RC_NIL, "encrypt_data");
   if (e) {
     uint8_t nonce[24], hdr[32];
@@ -143,7 +149,7 @@ int main(void) {
     rc_encrypter_free(e);
   }
   boxes[6] = (box){rnd, 10, 0, RC_EOF, 0, 0};
-  e = rc_encrypt_data(c, mkReader(7, 0), NULL, &err);
+  e = gpucipher_encrypt(c, 7, NULL, &err);
   CHECK(!e && err == RC_ERR_SHORT_NONCE, "short read of nonce");
 
   /* host-only name modes: obfuscate round trip, base32 encoding */
@@ -178,6 +184,18 @@ int main(void) {
   CHECK(bl == 8 && !memcmp(b32, "d1imor3f", 8), "base32 encode");
   CHECK(strcmp(rc_error_string(RC_ERR_BAD_BLOCK), "failed to authenticate decrypted block - bad password?") == 0,
         "error string");
+  /* keys derived on the Go side (Cipher.Key) installed directly */
+  rc_cipher *z = rc_cipher_new(NULL, NULL, &err);
+  CHECK(z && err == RC_NIL, "rc_cipher_new(NULL)");
+  if (z) {
+    uint8_t d2[32], n2[32], t2[16];
+    rc_cipher_keys(z, d2, n2, t2);
+    CHECK(d2[0] == 0 && d2[31] == 0, "empty password: zero keys");
+    rc_cipher_set_keys(z, dk, nk, nt);
+    rc_cipher_keys(z, d2, n2, t2);
+    CHECK(!memcmp(d2, dk, 32) && !memcmp(n2, nk, 32) && !memcmp(t2, nt, 16), "rc_cipher_set_keys");
+    rc_cipher_free(z);
+  }
   rc_cipher_free(c);
   if (failures) return 1;
   printf("c client ok\n");
