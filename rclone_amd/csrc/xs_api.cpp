@@ -249,8 +249,9 @@ int xs_fill_blocks_dev(void* d, uint64_t nblocks, uint64_t first_block, uint64_t
 
 void* xs_host_alloc(size_t bytes) {
   void* p = nullptr;
-  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) {
-    set_error("hipHostMalloc(%zu) failed", bytes);
+  const hipError_t e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable);
+  if (e != hipSuccess) {
+    set_error("hipHostMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
     return nullptr;
   }
   return p;

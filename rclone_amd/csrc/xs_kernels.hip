@@ -51,6 +51,9 @@
 #ifndef XS_FUSED_MAX  // single-request descriptor batches up to this many blocks: keygen + crypt in one launch
 #define XS_FUSED_MAX 16
 #endif
+#ifndef XS_FUSED_V  // fused kernel: 1 = keygen then split crypt, 2 = key schedule overlapped with the keystream
+#define XS_FUSED_V 2
+#endif
 #ifndef XS_KEYGEN_WIDE_MAX  // batches up to this many blocks get one keygen wave per block (latency)
 #define XS_KEYGEN_WIDE_MAX 16
 #endif
@@ -114,9 +117,32 @@ __device__ __forceinline__ void salsa_rounds_n(uint32_t (&x)[16], int nd) {
 }
 
 __device__ __forceinline__ void salsa_rounds(uint32_t (&x)[16]) { salsa_rounds_n(x, 10); }
+
+// The same 20 rounds through the deferred-XOR double rounds of xs_salsa_lazy.h.  For one state in
+// one wave (latency, not throughput: HSalsa20 and the keystream blocks of keygen_wave) the plain
+// form is compiled into a single dependent chain (~4 us); this one schedules as ~2 us.
+__device__ __forceinline__ void salsa_rounds_lazy(uint32_t (&x)[16]) {
+  uint32_t t[16];
+  xs_salsa_dr_lazy_enter(x, t);
+#pragma unroll 1
+  for (int i = 0; i < 9; i++) xs_salsa_dr_lazy(x, t);
+#pragma unroll
+  for (int i = 0; i < 16; i++)
+    if ((XS_LAZY_MASK >> i) & 1u) x[i] ^= t[i];
+}
 __device__ __forceinline__ void salsa_rounds9(uint32_t (&x)[16]) { salsa_rounds_n(x, 9); }
 
 constexpr uint32_t SIG0 = 0x61707865u, SIG1 = 0x3320646eu, SIG2 = 0x79622d32u, SIG3 = 0x6b206574u;
+
+// A wave-uniform value handed to the compiler as lane-varying: the computation that follows runs
+// on the VALU instead of the scalar unit.  For a latency-bound single state (HSalsa20 of a ranged
+// read's block) the SALU is ~3x slower: no one-instruction rotate, one scalar op in flight per
+// wave (measured 6.8 us vs ~2 us for the 20 rounds, tools/fused_probe.cpp).
+__device__ __forceinline__ uint32_t as_varying(uint32_t x) {
+  uint32_t v;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "v"(x));
+  return v;
+}
 
 // Salsa20/20 keystream block `ctr` for a 32-byte key (k[8]) and 8-byte nonce (n0, n1).
 // Salsa20/20 keystream block `ctr` for a 32-byte key (k[8]) and 8-byte nonce (n0, n1).
@@ -141,6 +167,18 @@ __device__ __forceinline__ void salsa20_block(const uint32_t (&k)[8], uint32_t n
   out[13] = x[13] + k[6];
   out[14] = x[14] + k[7];
   out[15] = x[15] + SIG3;
+}
+
+// salsa20_block with the rounds of salsa_rounds_lazy (latency-bound single states).
+__device__ __forceinline__ void salsa20_block_lazy(const uint32_t (&k)[8], uint32_t n0, uint32_t n1, uint32_t ctr,
+                                                   uint32_t (&out)[16]) {
+  const uint32_t in[16] = {SIG0, k[0], k[1], k[2], k[3], SIG1, n0, n1, ctr, 0u, SIG2, k[4], k[5], k[6], k[7], SIG3};
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) x[i] = in[i];
+  salsa_rounds_lazy(x);
+#pragma unroll
+  for (int i = 0; i < 16; i++) out[i] = x[i] + in[i];
 }
 
 // First double round, partially evaluated.  With key and nonce wave-uniform only the block
@@ -593,6 +631,85 @@ __device__ void full_corr(bool seal, P5 sumA, P5 sumB, P5 sumC, P5 sumD4, const 
   put5(o->corr, c);
 }
 
+// full_corr spread over the lanes of one wave (keygen_wave, latency): lanes 0..3 form the four
+// table sums at once, then the three independent product chains of corr -- S (lane 0), E*SW - B
+// (lane 1) and 2^128 (r^65 + r^66) [+ the SEAL key-slot words] times W63 (lane 2; lanes 3, 4 the
+// key-slot products) -- run in the same instructions; lane 0 combines.  pw[l] holds lane l's
+// table entry (C = lanes 0..7, D = 9..17, A = 18..25, B = 27..34, W63 = 36, r^65 = 37, r^66 = 38).
+// Same operations and canonicalisations as full_corr, so corr is bit-identical.
+__device__ __forceinline__ P5 shfl5(const P5& v, uint32_t src) {
+  P5 o;
+#pragma unroll
+  for (int i = 0; i < 5; i++) o.v[i] = (uint32_t)__shfl((int)v.v[i], (int)src);
+  return o;
+}
+__device__ __forceinline__ P5 sel5(bool c, const P5& a, const P5& b) {
+  P5 o;
+#pragma unroll
+  for (int i = 0; i < 5; i++) o.v[i] = c ? a.v[i] : b.v[i];
+  return o;
+}
+__device__ __forceinline__ P5 lds5(const uint32_t (*pw)[5], uint32_t k) {
+  P5 o;
+#pragma unroll
+  for (int i = 0; i < 5; i++) o.v[i] = pw[k][i];
+  return o;
+}
+
+__device__ __forceinline__ void full_corr_wave(bool seal, uint32_t l, const uint32_t (*pw)[5], const uint32_t (&ks)[16],
+                                               BlockKey* __restrict__ o) {
+  // table sums: lane 0 sum C, lane 1 sum A, lane 2 sum B, lane 3 D0..D3
+  const uint32_t base = l == 0u ? 0u : l == 1u ? 18u : l == 2u ? 27u : 9u;
+  const uint32_t cnt = l == 3u ? 4u : 8u;
+  P5 sum;
+#pragma unroll
+  for (int i = 0; i < 5; i++) sum.v[i] = 0;
+  if (l < 4u) {
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++)
+      if (k < cnt) add5(sum, lds5(pw, base + k));
+  }
+  pnorm(sum);
+  const P5 sumB = shfl5(sum, 2u), sumD4 = shfl5(sum, 3u);
+  const P5 r3 = lds5(pw, 3), r32 = lds5(pw, 13), W63 = lds5(pw, 36), r65 = lds5(pw, 37), r66 = lds5(pw, 38);
+  P5 E, B, two128, r6566 = r65;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    E.v[i] = kE[i];
+    B.v[i] = kB[i];
+    two128.v[i] = 0;
+  }
+  two128.v[4] = 1u << 24;  // 2^128 = 2^(104 + 24)
+  add5(r6566, r66);
+  pnorm(r6566);
+  // step 1: r3*sumC | sumA*sumB | 2^128 (r65 + r66) | key slot lo * r66 | key slot hi * r65
+  P5 x = sel5(l == 0u, r3, sel5(l == 1u, sum, sel5(l == 2u, two128, sel5(l == 3u, chunk26(ks[0], ks[1], ks[2], ks[3]),
+                                                                               chunk26(ks[4], ks[5], ks[6], ks[7])))));
+  P5 y = sel5(l == 0u, sum, sel5(l == 1u, sumB, sel5(l == 2u, r6566, sel5(l == 3u, r66, r65))));
+  P5 t = pmul(x, y);
+  // step 2: (r3 sumC) sumD4 | E * SW | kk * W63
+  const P5 t3 = shfl5(t, 3u), t4 = shfl5(t, 4u);
+  P5 kk = t;
+  if (seal) {
+    add5(kk, t3);
+    add5(kk, t4);
+    pnorm(kk);
+  }
+  x = sel5(l == 0u, t, sel5(l == 1u, E, kk));
+  y = sel5(l == 0u, sumD4, sel5(l == 1u, pcanon(t), W63));
+  t = pmul(x, y);
+  // step 3: S = (..) (1 + r^32) on lane 0; es_b (lane 1) and b (lane 2) canonicalised
+  P5 one_r32 = r32;
+  one_r32.v[0] += 1;
+  const P5 es_b = pcanon(psub(pcanon(t), B));
+  const P5 bb = pcanon(t);
+  const P5 S = pcanon(pmul(t, one_r32));
+  // step 4: a = S * es_b, corr = a - b
+  const P5 a = pcanon(pmul(S, shfl5(es_b, 1u)));
+  const P5 c = pcanon(psub(a, shfl5(bb, 2u)));
+  if (l == 0u) put5(o->corr, c);
+}
+
 // ---------------------------------------------------------------- keygen
 // One lane per crypt block.  MODE: 0 object seal, 1 object open, 2 descriptor seal,
 // 3 descriptor open.  Object mode derives nonce, offsets and length from the block
@@ -740,6 +857,20 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
 // is canonical, so tags and ciphertext equal the narrow keygen's.
 // The body: one wave (lanes l = threadIdx.x & 63) builds block b's key schedule into *o (global
 // memory, or LDS in the fused kernels); pw = 64 x 5 words of LDS scratch private to the wave.
+#ifdef XS_F2_PROBE
+extern __device__ unsigned long long xs_f2_probe[2 * 8 * 16];
+#define KG_MARK(slot)                                                                              \
+  do {                                                                                             \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
+    const unsigned long long c_ = __builtin_amdgcn_s_memtime();                                    \
+    if (blockIdx.x == 0 && (threadIdx.x >> 6) == 4 && l < 2u) xs_f2_probe[128 * l + 16 * 5 + (slot)] = l ? c_ : t_; \
+  } while (0)
+#else
+#define KG_MARK(slot) \
+  do {                \
+  } while (0)
+#endif
+
 template <int MODE>
 __device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& nonce0, uint64_t first_block,
                                             uint64_t total_len, const xs_block_desc* __restrict__ desc,
@@ -757,10 +888,15 @@ __device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& n
   }
   uint32_t x[16] = {SIG0, key.k[0], key.k[1], key.k[2], key.k[3], SIG1, n[0], n[1],
                     n[2], n[3],     SIG2,     key.k[4], key.k[5], key.k[6], key.k[7], SIG3};
-  salsa_rounds(x);
+#pragma unroll
+  for (int i = 0; i < 16; i++) x[i] = as_varying(x[i]);  // HSalsa20 on the VALU (latency)
+  KG_MARK(0);
+  salsa_rounds_lazy(x);
+  KG_MARK(1);
   uint32_t sk[8] = {x[0], x[5], x[10], x[15], x[6], x[7], x[8], x[9]};
   uint32_t ks[16];
-  salsa20_block(sk, n[4], n[5], l < 32 ? 0u : 1024u, ks);
+  salsa20_block_lazy(sk, n[4], n[5], l < 32 ? 0u : 1024u, ks);
+  KG_MARK(2);
   if (l == 32 && len > XS_BLOCK_DATA - 32) {
 #pragma unroll
     for (int i = 0; i < 8; i++) o->ks1024[i] = ks[i];
@@ -812,6 +948,7 @@ __device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& n
         const P5 q = pmul(a, c);
         if (act) p = q;
       }
+      KG_MARK(3 + m);
       if (m < 3) {  // next level: base^0 = 1, base^1 = this level's base^8
         P5 nb;
 #pragma unroll
@@ -832,6 +969,7 @@ __device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& n
       const P5 q = pmul(a, c);
       if (l >= 36u && l <= 38u) p = q;
     }
+    KG_MARK(7);
     if (l < 8) put5(o->full.C[l], p);
     else if (l >= 9 && l < 18) put5(o->full.D[l - 9], p);
     else if (l >= 18 && l < 26) put5(o->full.A[l - 18], p);
@@ -841,25 +979,9 @@ __device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& n
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (l == 0) {
-      P5 sumA, sumB, sumC, sumD4, v[5];
-#pragma unroll
-      for (int i = 0; i < 5; i++) {
-        sumC.v[i] = sumD4.v[i] = sumA.v[i] = sumB.v[i] = 0;
-        for (int k = 0; k < 8; k++) {
-          sumC.v[i] += pw[k][i];
-          sumA.v[i] += pw[18 + k][i];
-          sumB.v[i] += pw[27 + k][i];
-        }
-        for (int k = 0; k < 4; k++) sumD4.v[i] += pw[9 + k][i];
-        v[0].v[i] = pw[3][i];   // r^3
-        v[1].v[i] = pw[13][i];  // r^32 = D[4]
-        v[2].v[i] = pw[37][i];  // r^65
-        v[3].v[i] = pw[38][i];  // r^66
-        v[4].v[i] = pw[36][i];  // r^4032
-      }
-      full_corr(MODE == 0 || MODE == 2, sumA, sumB, sumC, sumD4, v[0], v[1], v[2], v[3], v[4], ks, o);
-    }
+    KG_MARK(8);
+    full_corr_wave(MODE == 0 || MODE == 2, l, pw, ks, o);
+    KG_MARK(9);
     return;
   }
   // partial blocks (one per object at most): lane e's entry by square-and-multiply
@@ -1606,6 +1728,369 @@ __global__ void __launch_bounds__(256) xs_crypt_fused(KeyArg key, NonceArg bound
   }
 }
 
+// Tiny descriptor batches, latency-first (XS_FUSED_V 2, default): one workgroup per block, five
+// waves.  For a full block, waves 0..3 start at once on the data: each stages its four 4 KiB
+// groups with LDS-DMA right after the descriptor read (one PCIe round trip for all of them),
+// computes the HSalsa20 subkey itself and runs its four keystream blocks per lane, writing the
+// output and keeping the ciphertext in LDS; wave 4 meanwhile builds the block's key schedule
+// (keygen_wave: Poly1305 key, power tables, correction term) and the shared Toeplitz digit
+// table, at raised issue priority (it shares wave 0's SIMD, which therefore takes one group and
+// waves 1..3 five each).  After one barrier the four waves run the matrix-core Poly1305 over their LDS-resident
+// ciphertext (phase 2), their accumulators are summed through LDS and wave 0 finalises as
+// crypt_block_mfma does.  The key schedule thus leaves the critical path instead of preceding
+// the whole block.  Partial blocks take the fused-v1 order (keygen, then wave 0's VALU path).
+// Groups per crypt wave: wave 0 also shares its SIMD with the key-schedule wave, so it takes one
+// group and waves 1..3 five each (the key schedule is the longer chain, tools/fused_probe.cpp).
+__device__ __forceinline__ uint32_t f2_first(uint32_t w) { return w == 0u ? 0u : 5u * w - 4u; }
+__device__ __forceinline__ uint32_t f2_count(uint32_t w) { return w == 0u ? 1u : 5u; }
+constexpr int F2_STAGE = 5 * 1024;  // words of staging per crypt wave: up to 5 groups of 4 KiB
+constexpr int F2_LDS_WORDS = 4 * F2_STAGE + 4 * 1024 + 3 * 2048 + 64 * 12;  // stage, relay, acc exchange, Z
+
+#ifdef XS_F2_PROBE
+// Diagnostic build only (tools/fused_probe.cpp): s_memrealtime (100 MHz) at phase boundaries, per
+// wave of workgroup 0, lane-indexed vector stores.
+__device__ unsigned long long xs_f2_probe[2 * 8 * 16];
+#define F2_MARK(slot)                                                                        \
+  do {                                                                                       \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                          \
+    const unsigned long long c_ = __builtin_amdgcn_s_memtime();                              \
+    if (blockIdx.x == 0 && l < 2u) xs_f2_probe[128 * l + 16 * wave + (slot)] = l ? c_ : t_;   \
+  } while (0)
+#else
+#define F2_MARK(slot) \
+  do {                \
+  } while (0)
+#endif
+
+template <bool SEAL>
+__global__ void __launch_bounds__(320) xs_crypt_fused2(KeyArg key, NonceArg bounds, const xs_block_desc* __restrict__ desc,
+                                                       uint64_t nblocks, const uint8_t* __restrict__ src,
+                                                       uint8_t* __restrict__ dst, uint8_t* __restrict__ ok,
+                                                       uint32_t* __restrict__ ctr, uint32_t* __restrict__ flag,
+                                                       uint32_t seq) {
+  constexpr int MODE = SEAL ? 2 : 3;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[F2_LDS_WORDS];
+  __shared__ BlockKey kl;
+  __shared__ uint32_t pw[64][5];
+  if (blockIdx.x >= nblocks) return;  // uniform per workgroup (grid == nblocks)
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63u;
+  const uint64_t blk = blockIdx.x;
+  F2_MARK(0);
+  uint32_t nn[6];
+  uint64_t soff, doff;
+  uint32_t len;
+  const bool valid = block_params<MODE>(bounds, 0, 0, desc, blk, nn, soff, doff, len);
+  // The descriptor is uniform: move it into SGPRs now.  vmcnt drains in order, so a later use of
+  // a descriptor word still in a VGPR would make the compiler wait for every data load of the
+  // block issued after it.
+#pragma unroll
+  for (int i = 0; i < 6; i++) nn[i] = __builtin_amdgcn_readfirstlane(nn[i]);
+  // (readfirstlane returns int: both halves go through uint32_t, or an offset with bit 31 set
+  // in its low word would sign-extend over the high word)
+  soff = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(soff >> 32)) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)soff);
+  doff = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(doff >> 32)) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)doff);
+  len = __builtin_amdgcn_readfirstlane(len);
+  F2_MARK(1);
+  if (!valid || len != XS_BLOCK_DATA) {
+    // rejected descriptor or partial block: the fused-v1 order (wave 4 idles)
+    if (wave == 0) keygen_wave<MODE>(key, bounds, 0, 0, desc, blk, &kl, pw);
+    __syncthreads();
+    if (wave < 4) crypt_wave<SEAL, 4, true>(&kl, nblocks, src, dst, ok, lds);
+  } else {
+    uint32_t* const stage = lds;                      // [4][4096]
+    uint32_t* const relay = lds + 4 * F2_STAGE;       // [4][1024]: OPEN output relayout; wave 0's transpose
+    uint32_t* const xacc = relay + 4 * 1024;          // [3][2048]: accumulators of waves 1..3
+    uint32_t* const zt = xacc + 3 * 2048;             // [64][12]: Toeplitz digit rows
+    const uint8_t* in = src + soff;
+    uint8_t* out = dst + doff;
+    const uint8_t* pin = SEAL ? in : in + XS_BLOCK_HDR;
+    uint8_t* pout = SEAL ? out + XS_BLOCK_HDR : out;
+    const uint8_t* pin_m32 = pin - 32;
+    uint8_t* pout_m32 = pout - 32;
+    const uint32_t lane_off = 16u * (4u * (l & 15u) + (l >> 4));
+    const bool not_key = (l & 47u) != 0u;
+    const uint32_t n = l & 15u, kg = l >> 4;
+    uint4 tail[2];  // wave 0 lane 63: chunks 4094, 4095 (fetched early, used in the finalisation)
+    if (wave < 4) {
+      // ---- phase 1: stage all four groups, keystream + XOR + output, ciphertext kept in LDS
+      uint32_t* const sw = stage + F2_STAGE * wave;
+      if (wave == 0 && l == 0u) {  // key slots (chunks -2, -1): never loaded or stored
+        *reinterpret_cast<uint4*>(sw) = make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(sw + 64) = make_uint4(0u, 0u, 0u, 0u);
+      }
+      const uint32_t g0 = f2_first(wave), gn = f2_count(wave);
+#pragma unroll
+      for (uint32_t g = 0; g < 5; g++) {
+        if (g >= gn) break;
+        const uint32_t u = g0 + g;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (j > 0 || u > 0 || not_key)
+            __builtin_amdgcn_global_load_lds(pin_m32 + 4096u * u + lane_off + 1024 * j,
+                                             (lds_void*)(sw + 1024 * g + 256 * j), 16, 0, 0);
+      }
+      if (wave == 0) {  // every lane loads the same two chunks (lane 63 uses them); a lane-varying
+                        // zero keeps them VGPR loads that nothing waits for before the finalisation
+        const uint8_t* tp = pin + 16u * 4094u + as_varying(0u);
+        tail[0] = *reinterpret_cast<const uint4*>(tp);
+        tail[1] = *reinterpret_cast<const uint4*>(tp + 16);
+      }
+      F2_MARK(14);
+      uint32_t x[16] = {SIG0, key.k[0], key.k[1], key.k[2], key.k[3], SIG1, nn[0], nn[1],
+                        nn[2], nn[3],     SIG2,     key.k[4], key.k[5], key.k[6], key.k[7], SIG3};
+#pragma unroll
+      for (int i = 0; i < 16; i++) x[i] = as_varying(x[i]);  // on the VALU: see as_varying
+      salsa_rounds_lazy(x);  // HSalsa20 (each crypt wave derives the subkey itself: no wait on wave 4)
+      F2_MARK(15);
+      const uint32_t sk[8] = {x[0], x[5], x[10], x[15], x[6], x[7], x[8], x[9]};
+      const SalsaPre pre = salsa_pre(sk, nn[4], nn[5]);
+      F2_MARK(2);
+      uint32_t* const rl = relay + 1024 * wave;
+#pragma unroll 1
+      for (uint32_t g = 0; g < gn; g++) {
+        const uint32_t u = g0 + g;
+        uint32_t ks[16];
+        salsa20_block_pre(pre, 64u * u + l, ks);
+        F2_MARK(3 + 2 * g);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        F2_MARK(4 + 2 * g);
+        uint32_t* sb = sw + 1024 * g;
+        uint4* mine = reinterpret_cast<uint4*>(sb + 256 * (l >> 4) + 4 * (l & 15u));
+        uint32_t o[16];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint4 v = mine[16 * j];
+          o[4 * j] = v.x ^ ks[4 * j];
+          o[4 * j + 1] = v.y ^ ks[4 * j + 1];
+          o[4 * j + 2] = v.z ^ ks[4 * j + 2];
+          o[4 * j + 3] = v.w ^ ks[4 * j + 3];
+        }
+        // SEAL: the ciphertext replaces the plaintext in the stage; OPEN: the stage keeps the
+        // ciphertext and the plaintext is laid out through the relay slot
+        uint32_t* lay = SEAL ? sb : rl;
+        uint4* lmine = reinterpret_cast<uint4*>(lay + 256 * (l >> 4) + 4 * (l & 15u));
+#pragma unroll
+        for (int j = 0; j < 4; j++) lmine[16 * j] = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
+        asm volatile("" ::: "memory");  // LDS ops of one wave execute in order
+        uint4 w[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) w[j] = *reinterpret_cast<const uint4*>(lay + 256 * j + 4 * l);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (j > 0 || u > 0 || not_key)
+            *reinterpret_cast<uint4*>(pout_m32 + 4096u * u + lane_off + 1024 * j) = w[j];
+      }
+      if (!SEAL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // plaintext out before any zero-fill
+      F2_MARK(11);
+    } else {
+      // ---- wave 4: key schedule into LDS, then the shared Toeplitz digit table.  It shares a
+      // SIMD with wave 0 and is the longer chain: it issues first.
+      __builtin_amdgcn_s_setprio(3);
+      keygen_wave<MODE>(key, bounds, 0, 0, desc, blk, &kl, pw);
+      F2_MARK(2);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      P5 qa, qb;
+      const uint32_t k = 63u - l;
+#pragma unroll
+      for (int i = 0; i < 5; i++) {
+        qa.v[i] = kl.full.A[k & 7u][i];
+        qb.v[i] = kl.full.B[k >> 3][i];
+      }
+      const P32 wq = to32(pmul(qa, qb));
+      uint32_t w0 = wq.w0, w1 = wq.w1, w2 = wq.w2, w3 = wq.w3, w4 = wq.w4;
+      unsigned cy;
+      w0 = __builtin_addc(w0, 0x80808080u, 0u, &cy);
+      w1 = __builtin_addc(w1, 0x80808080u, cy, &cy);
+      w2 = __builtin_addc(w2, 0x80808080u, cy, &cy);
+      w3 = __builtin_addc(w3, 0x80808080u, cy, &cy);
+      w4 = (w4 + 0x80u + cy) ^ 0x80u;
+      w0 ^= 0x80808080u;
+      w1 ^= 0x80808080u;
+      w2 ^= 0x80808080u;
+      w3 ^= 0x80808080u;
+      uint4* row = reinterpret_cast<uint4*>(zt + 12u * l);
+      row[0] = make_uint4(0u, 0u, 0u, w4 << 24);
+      row[1] = make_uint4(__builtin_bswap32(w3), __builtin_bswap32(w2), __builtin_bswap32(w1), __builtin_bswap32(w0));
+      row[2] = make_uint4(0u, 0u, 0u, 0u);
+      F2_MARK(3);
+    }
+    __syncthreads();  // B1: key schedule, Z table and every wave's staged ciphertext are in LDS
+    F2_MARK(12);
+    xs_v4i acc[4][2];
+    if (wave < 4) {
+      // ---- phase 2: matrix-core Poly1305 over the LDS-resident ciphertext
+      const uint32_t zlo = (15u - n) >> 2, zsh = (31u - n) & 3u;
+      uint32_t zaddr = (uint32_t)(uintptr_t)((const lds_u32*)zt + 12u * kg + zlo);
+      asm volatile("" : "+v"(zaddr));
+      const lds_u32* zl = (const lds_u32*)(uintptr_t)zaddr;
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) acc[j][mt][i] = wave == 0 ? 1 << 24 : 0;  // the bias once per block
+      const uint32_t* sw = stage + F2_STAGE * wave;
+      const uint32_t g0 = f2_first(wave), gn = f2_count(wave);
+#pragma unroll 1
+      for (uint32_t g = 0; g < gn; g++) {
+        const uint32_t u = g0 + g;
+        const uint4* mine = reinterpret_cast<const uint4*>(sw + 1024 * g + 256 * (l >> 4) + 4 * (l & 15u));
+        uint32_t cw[16];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint4 v = mine[16 * j];
+          cw[4 * j] = v.x; cw[4 * j + 1] = v.y; cw[4 * j + 2] = v.z; cw[4 * j + 3] = v.w;
+        }
+        const lds_u32* zr = zl + 48u * u;
+        uint32_t z[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) z[i] = zr[i];
+        xs_v4i A[2];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          A[1][i] = (int)__builtin_amdgcn_alignbyte(z[i + 1], z[i], zsh);
+          A[0][i] = (int)__builtin_amdgcn_alignbyte(z[i + 5], z[i + 4], zsh);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          xs_v4i B;
+#pragma unroll
+          for (int i = 0; i < 4; i++) B[i] = (int)(cw[4 * j + i] ^ 0x80808080u);
+#pragma unroll
+          for (int mt = 0; mt < 2; mt++) acc[j][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[mt], B, acc[j][mt], 0, 0, 0);
+        }
+      }
+      if (wave > 0) {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+          for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) xacc[(wave - 1u) * 2048u + (uint32_t)(8 * j + 4 * mt + i) * 64u + l] = acc[j][mt][i];
+      }
+    }
+    __syncthreads();  // B2: the other waves' accumulators are in LDS
+    F2_MARK(13);
+    if (wave == 0) {
+#pragma unroll
+      for (int w = 0; w < 3; w++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+          for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) acc[j][mt][i] += (int)xacc[(uint32_t)w * 2048u + (uint32_t)(8 * j + 4 * mt + i) * 64u + l];
+      // transpose the partial words through wave 0's relay slot (as crypt_block_mfma)
+      uint64_t* t64 = reinterpret_cast<uint64_t*>(relay);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        uint64_t sx[2];
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+          sx[mt] = (uint64_t)(uint32_t)acc[j][mt][0] + ((uint64_t)(uint32_t)acc[j][mt][1] << 8) +
+                   ((uint64_t)(uint32_t)acc[j][mt][2] << 16) + ((uint64_t)(uint32_t)acc[j][mt][3] << 24);
+        *reinterpret_cast<ulonglong2*>(t64 + (((n * 4u + j) * 4u + kg) * 2u)) = make_ulonglong2(sx[0], sx[1]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      uint64_t xw[8];
+      {
+        const uint64_t* rd = t64 + (n * 4u + kg) * 8u;
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) {
+          const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(rd + 2 * kk);
+          xw[kk] = v.x;
+          xw[4 + kk] = v.y;
+        }
+      }
+      const BlockKey* bk = &kl;
+      P5 hs;
+      {
+        const P5 V = column_value(xw);
+        const uint32_t e = 66u - (4u * n + kg);
+        P5 t1, t2;
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          t1.v[i] = bk->full.C[e & 7u][i];
+          t2.v[i] = bk->full.D[e >> 3][i];
+        }
+        hs = pmul(V, pmul(t2, t1));
+      }
+      if (l == 0u) {
+#pragma unroll
+        for (int i = 0; i < 5; i++) hs.v[i] += bk->corr[i];
+      }
+      if (l == 63u) {  // chunks 4094, 4095 (keystream block 1024 words 0..7): exponents 2 and 1
+        P5 rr, tl;
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          rr.v[i] = bk->r[i];
+          tl.v[i] = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          const uint32_t w[4] = {tail[j].x, tail[j].y, tail[j].z, tail[j].w};
+          uint32_t o4[4];
+#pragma unroll
+          for (int i = 0; i < 4; i++) o4[i] = w[i] ^ bk->ks1024[4 * j + i];
+          *reinterpret_cast<uint4*>(pout + 16u * (4094u + j)) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+          const uint32_t* cw = SEAL ? o4 : w;
+          padd_full(tl, cw[0], cw[1], cw[2], cw[3]);
+          tl = pmul(tl, rr);
+        }
+#pragma unroll
+        for (int i = 0; i < 5; i++) hs.v[i] += tl.v[i];
+      }
+      pnorm(hs);
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+        for (int i = 0; i < 5; i++) hs.v[i] += (uint32_t)__shfl_xor((int)hs.v[i], off, 64);
+        if (off == 2) pnorm(hs);
+      }
+      uint32_t verdict = 1;
+      if (l == 0) {
+        const P5 hc = pcanon(hs);
+        const uint32_t s4[4] = {bk->s[0], bk->s[1], bk->s[2], bk->s[3]};
+        uint32_t tag[4];
+        ptag(hc, s4, tag);
+        if (SEAL) {
+          *reinterpret_cast<uint4*>(out) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+        } else {
+          const uint4 want = *reinterpret_cast<const uint4*>(in);
+          const uint32_t diff = (want.x ^ tag[0]) | (want.y ^ tag[1]) | (want.z ^ tag[2]) | (want.w ^ tag[3]);
+          verdict = diff == 0 ? 1u : 0u;
+          ok[blk] = diff == 0 ? 1 : 0;
+        }
+      }
+      if (!SEAL) {
+        verdict = (uint32_t)__shfl((int)verdict, 0, 64);
+        if (verdict == 0) {  // authentication failed: zero the block (every wave's stores are done, B2)
+          __builtin_amdgcn_s_waitcnt(0);
+          for (uint32_t off = 16u * l; off < XS_BLOCK_DATA; off += 16u * LANES)
+            *reinterpret_cast<uint4*>(pout + off) = make_uint4(0, 0, 0, 0);
+        }
+      }
+      F2_MARK(14);
+    }
+  }
+  if (ctr) {  // completion word: every wave's outputs at system scope, then the last workgroup signals
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == (uint32_t)nblocks - 1u) {
+        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence_system();
+        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) xs_seal_split(const BlockKey* __restrict__ keys, uint64_t nblocks,
                                                      const uint8_t* __restrict__ src, uint8_t* __restrict__ dst) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
@@ -1695,6 +2180,15 @@ hipError_t launch_crypt_fused(bool seal, const KeyArg& key, const NonceArg& boun
                               uint64_t nblocks, const uint8_t* src, uint8_t* dst, uint8_t* ok, uint32_t* ctr,
                               uint32_t* flag, uint32_t seq, hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
+  static const int version = [] {  // env XS_FUSED_V: 1 = keygen then split crypt, 2 = overlapped (A/B)
+    const char* v = getenv("XS_FUSED_V");
+    return v ? atoi(v) : XS_FUSED_V;
+  }();
+  if (version >= 2) {
+    if (seal) hipLaunchKernelGGL(xs_crypt_fused2<true>, dim3((unsigned)nblocks), dim3(320), 0, stream, key, bounds, desc, nblocks, src, dst, ok, ctr, flag, seq);
+    else hipLaunchKernelGGL(xs_crypt_fused2<false>, dim3((unsigned)nblocks), dim3(320), 0, stream, key, bounds, desc, nblocks, src, dst, ok, ctr, flag, seq);
+    return hipGetLastError();
+  }
   if (seal) hipLaunchKernelGGL(xs_crypt_fused<true>, dim3((unsigned)nblocks), dim3(256), 0, stream, key, bounds, desc, nblocks, src, dst, ok, ctr, flag, seq);
   else hipLaunchKernelGGL(xs_crypt_fused<false>, dim3((unsigned)nblocks), dim3(256), 0, stream, key, bounds, desc, nblocks, src, dst, ok, ctr, flag, seq);
   return hipGetLastError();

@@ -83,6 +83,9 @@ int xs_engine_open(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24]
                    const void* body, uint64_t body_len, void* plain, uint8_t* ok) {
   std::lock_guard<std::mutex> g(e->mu);
   e->calls++;
+  if (getenv("STUB_TRACE"))
+    fprintf(stderr, "open fb=%llu len=%llu in%%16=%u out%%16=%u\n", (unsigned long long)first_block,
+            (unsigned long long)body_len, (unsigned)((uintptr_t)body & 15u), (unsigned)((uintptr_t)plain & 15u));
   const uint8_t* in = (const uint8_t*)body;
   uint8_t* out = (uint8_t*)plain;
   for (uint64_t j = 0; j * XS_BLOCK_SIZE < body_len; j++) {

@@ -1,6 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-R=$(pwd)
-export TMPDIR=/tmp
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/r02j.prof -- python3 $R/bench.py --no-cpu > $R/gpurun_out/r02j.prof.log 2>&1 || { echo PROF_FAILED; tail $R/gpurun_out/r02j.prof.log; exit 1; }
-tail -1 $R/gpurun_out/r02j.prof.log | cut -c1-300
+bash tools/fused_v_ab_mt.sh > gpurun_out/fvmt.log 2>&1 || { echo AB_FAILED; tail -20 gpurun_out/fvmt.log; exit 1; }
+for f in gpurun_out/fvmt_*.json gpurun_out/fvmtprof_*.json; do echo $f $(python3 -c "import json,sys; d=json.load(open('$f')); print(d['p50_us'], d['p99_us'], d['reads_per_s'], d['bad'])"); done

@@ -118,7 +118,15 @@ int main(int argc, char** argv) {
       rc_decrypter_free(d);
     }
     const double dt = now() - t0;
-    if (got != len || memcmp(buf.data(), plain.data() + off, (size_t)len)) bad++;
+    if (got != len || memcmp(buf.data(), plain.data() + off, (size_t)len)) {
+      if (bad++ < 4) {
+        int64_t first = -1;
+        for (int64_t i = 0; i < got && first < 0; i++)
+          if (buf[(size_t)i] != plain[(size_t)(off + i)]) first = i;
+        fprintf(stderr, "bad read: off %lld got %lld err %d (%s) first mismatch %lld xs: %s\n", (long long)off,
+                (long long)got, (int)e, rc_error_string(e), (long long)first, xs_last_error());
+      }
+    }
     return dt;
   };
   {  // warm-up (engine creation, first launches)
