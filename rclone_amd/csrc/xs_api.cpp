@@ -320,7 +320,11 @@ struct xs_engine {
     uint64_t blocks = 0;
     int rc = XS_OK;
   };
-  std::vector<CSlot> cslots;
+  std::vector<CSlot> cslots;  // [0, ncslots): the leader's ring; then the express lanes
+  size_t ncslots = 0, nexpress = 2;
+  uint64_t express_max = 4;  // requests of at most this many blocks may take an express lane
+  std::atomic<uint32_t> express_busy{0};  // bit i: express lane i in use
+  std::atomic<uint64_t> st_express{0};
   uint64_t c_cap_blocks = 0, c_cap_bytes = 0;
   uint64_t st_batches = 0, st_reqs = 0, st_blocks = 0;
   std::atomic<uint64_t> st_host_md5_objs{0}, st_host_md5_bytes{0}, st_md5_objs{0};
@@ -457,9 +461,15 @@ extern "C" xs_engine* xs_engine_create(int device, uint32_t batch_blocks, int ns
   // (+16 bytes of alignment slack per block for the per-request 16-byte alignment)
   e->c_cap_blocks = batch_blocks;
   e->c_cap_bytes = (uint64_t)batch_blocks * (XS_BLOCK_SIZE + 16);
-  e->cslots.resize(nslots);
+  e->ncslots = (size_t)nslots;
+  if (const char* v = getenv("XS_EXPRESS_LANES")) e->nexpress = std::min<size_t>(strtoull(v, nullptr, 10), 8);
+  e->cslots.resize(e->ncslots + e->nexpress);
+  int prio_least = 0, prio_greatest = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
   for (auto& c : e->cslots) {
-    if (hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking) != hipSuccess ||
+    const bool express = &c >= &e->cslots[e->ncslots];
+    if ((express ? hipStreamCreateWithPriority(&c.s, hipStreamNonBlocking, prio_greatest)
+                 : hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking)) != hipSuccess ||
         hipEventCreateWithFlags(&c.done, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c.in, e->c_cap_bytes) != hipSuccess || hipMalloc(&c.out, e->c_cap_bytes) != hipSuccess ||
         hipMalloc(&c.ok, batch_blocks) != hipSuccess ||
@@ -488,6 +498,7 @@ extern "C" xs_engine* xs_engine_create(int device, uint32_t batch_blocks, int ns
   }
   if (const char* v = getenv("XS_ENGINE_COALESCE")) e->coalesce = atoi(v) != 0;
   if (const char* v = getenv("XS_ENGINE_ZERO_COPY")) e->zero_copy = atoi(v) != 0;
+  if (const char* v = getenv("XS_EXPRESS_MAX")) e->express_max = strtoull(v, nullptr, 10);
   return e;
 }
 
@@ -822,6 +833,39 @@ static int engine_issue_batch(xs_engine* e, xs_engine::CSlot& c) {
   return XS_OK;
 }
 
+// Wait for the combined batch in flight on c and hand its verdicts to the requests (zero-copy
+// batches); c.rc carries the outcome.  A fused batch stores its completion word (after its
+// outputs, system scope): poll it, falling back to the event if the stream ends (or fails)
+// without it.
+static void engine_wait_batch(xs_engine::CSlot& c) {
+  if (c.rc == XS_OK) {
+    bool seen = false;
+    if (c.spin) {
+      // bounded: a fused batch takes tens of microseconds; past kSpinNs (a busy GPU) the
+      // waiter blocks on the event instead of burning a core
+      const auto t0 = std::chrono::steady_clock::now();
+      for (unsigned k = 1;; k++) {
+        if (__atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) == c.seq) {
+          seen = true;
+          break;
+        }
+        __builtin_ia32_pause();
+        if ((k & 255u) == 0) {
+          if (hipEventQuery(c.done) != hipErrorNotReady) break;
+          if (std::chrono::steady_clock::now() - t0 > std::chrono::nanoseconds(kSpinNs)) break;
+        }
+      }
+    }
+    hipError_t err = seen ? hipSuccess : hipEventSynchronize(c.done);
+    if (err != hipSuccess) c.rc = hip_fail(err, "coalesced stream");
+  } else {
+    (void)hipStreamSynchronize(c.s);
+  }
+  if (c.rc == XS_OK && c.zc)
+    for (auto* q : c.batch)
+      if (!q->seal) memcpy(q->ok, c.h_ok + q->blk0, q->nblocks);
+}
+
 static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
                          const void* in, uint64_t in_len, void* out, uint8_t* ok, uint64_t nblocks) {
   xs_engine::Req req{};
@@ -840,6 +884,29 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
   req.zc = e->zero_copy && host_dev_ptr(in, &req.d_in, e->device) && host_dev_ptr(out, &req.d_out, e->device) &&
            !(req.d_in & 15u) && !(req.d_out & 15u);
   if (!req.zc) req.d_in = req.d_out = 0;
+  // Express lanes (XS_EXPRESS_LANES, default 2; XS_EXPRESS_MAX=0 turns them off): a small
+  // request (a stream's first one-block refill, a ranged read) launches at once on a lane of its
+  // own with a high-priority stream when one is free, instead of joining -- and waiting for --
+  // the combined batches of large requests in the leader's ring.
+  for (size_t x = 0; x < e->nexpress && nblocks <= e->express_max; x++) {
+    const uint32_t bit = 1u << x;
+    if (!(e->express_busy.fetch_or(bit, std::memory_order_acquire) & bit)) {
+      auto& c = e->cslots[e->ncslots + x];
+      c.batch.assign(1, &req);
+      c.blocks = nblocks;
+      c.rc = engine_issue_batch(e, c);
+      engine_wait_batch(c);
+      const int rc = c.rc;
+      c.batch.clear();
+      e->express_busy.fetch_and(~bit, std::memory_order_release);
+      e->st_express.fetch_add(1, std::memory_order_relaxed);
+      std::lock_guard<std::mutex> g(e->qmu);
+      e->st_batches++;
+      e->st_reqs++;
+      e->st_blocks += nblocks;
+      return rc;
+    }
+  }
   std::unique_lock<std::mutex> lk(e->qmu);
   e->queue.push_back(&req);
   while (!req.done) {
@@ -850,7 +917,7 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
     // lead: keep up to nslots combined batches in flight until our own request is done and
     // nothing is in flight, then hand over
     e->leader = true;
-    const size_t ns = e->cslots.size();
+    const size_t ns = e->ncslots;
     size_t head = 0, inflight = 0;  // ring of slots: [head, head + inflight) are in flight
     while (!(req.done && inflight == 0)) {
       if (inflight < ns && !e->queue.empty() && !req.done) {
@@ -871,34 +938,7 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
       if (inflight == 0) break;  // nothing queued for us (own request already done)
       auto& c = e->cslots[head];
       lk.unlock();
-      if (c.rc == XS_OK) {
-        // a fused batch stores its completion word (after its outputs, system scope): poll it,
-        // falling back to the event if the stream ends (or fails) without it
-        bool seen = false;
-        if (c.spin) {
-          // bounded: a fused batch takes tens of microseconds; past kSpinNs (a busy GPU) the
-          // leader blocks on the event instead of burning a core
-          const auto t0 = std::chrono::steady_clock::now();
-          for (unsigned k = 1;; k++) {
-            if (__atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) == c.seq) {
-              seen = true;
-              break;
-            }
-            __builtin_ia32_pause();
-            if ((k & 255u) == 0) {
-              if (hipEventQuery(c.done) != hipErrorNotReady) break;
-              if (std::chrono::steady_clock::now() - t0 > std::chrono::nanoseconds(kSpinNs)) break;
-            }
-          }
-        }
-        hipError_t err = seen ? hipSuccess : hipEventSynchronize(c.done);
-        if (err != hipSuccess) c.rc = hip_fail(err, "coalesced stream");
-      } else {
-        (void)hipStreamSynchronize(c.s);
-      }
-      if (c.rc == XS_OK && c.zc)
-        for (auto* q : c.batch)
-          if (!q->seal) memcpy(q->ok, c.h_ok + q->blk0, q->nblocks);
+      engine_wait_batch(c);
       lk.lock();
       for (auto* q : c.batch) {
         q->rc = c.rc;
