@@ -66,12 +66,19 @@ def parse():
 
 
 def cpu_baseline(seconds):
-    """Oracle (C restatement, OpenMP over blocks) seal+open of a bounded sample."""
+    """CPU restatement seal+open of a bounded sample, OpenMP over blocks: the vectorised one
+    (oracle/xsalsa_simd.c: AVX-512 16-way / AVX2 8-way Salsa20, radix-2^44 Poly1305) when the host
+    has AVX2, else the scalar oracle/xsalsa_oracle.c."""
     import numpy as np
     from oracle import pyoracle as orc  # checker/baseline only
     from rclone_amd.testdata import splitmix64_bytes
 
     lib = orc.lib()
+    level = lib.orc_simd_level()
+    seal, open_ = ((lib.orc_simd_seal_blocks, lib.orc_simd_open_blocks) if level > 0
+                   else (lib.orc_seal_blocks, lib.orc_open_blocks))
+    impl = {2: "oracle/xsalsa_simd.c AVX-512 (16-way Salsa20, radix-2^44 Poly1305)",
+            1: "oracle/xsalsa_simd.c AVX2 (8-way Salsa20, radix-2^44 Poly1305)"}.get(level, "oracle/xsalsa_oracle.c scalar")
     nb = 1024  # 64 MiB sample, repeated until `seconds` elapse
     plain = np.frombuffer(splitmix64_bytes(0x5EED, nb * BLOCK_DATA), dtype=np.uint8).copy()
     body = np.empty(nb * BLOCK_SIZE, dtype=np.uint8)
@@ -80,12 +87,12 @@ def cpu_baseline(seconds):
     key = splitmix64_bytes(1, 32)
     n0 = splitmix64_bytes(2, 24)
     vp = ctypes.c_void_p
-    threads = lib.orc_seal_blocks(vp(body.ctypes.data), vp(plain.ctypes.data), nb, n0, key)  # warm
+    threads = seal(vp(body.ctypes.data), vp(plain.ctypes.data), nb, n0, key)  # warm
     t0 = time.perf_counter()
     passes = 0
     while True:
-        threads = lib.orc_seal_blocks(vp(body.ctypes.data), vp(plain.ctypes.data), nb, n0, key)
-        lib.orc_open_blocks(vp(out.ctypes.data), vp(ok.ctypes.data), vp(body.ctypes.data), nb, n0, key)
+        threads = seal(vp(body.ctypes.data), vp(plain.ctypes.data), nb, n0, key)
+        open_(vp(out.ctypes.data), vp(ok.ctypes.data), vp(body.ctypes.data), nb, n0, key)
         passes += 1
         el = time.perf_counter() - t0
         if el >= seconds:
@@ -94,7 +101,7 @@ def cpu_baseline(seconds):
     gib = passes * 2 * nb * BLOCK_DATA / 2**30
     return {"value": round(gib / el, 3), "unit": "GiB/s", "cores": int(threads), "kind": "port",
             "sample": f"{passes} x (seal+open of {nb} x 64KiB blocks) = {gib:.1f} GiB in {el:.1f} s, "
-                      f"oracle/xsalsa_oracle.c OpenMP"}
+                      f"{impl}, OpenMP over blocks"}
 
 
 def load_traffic():

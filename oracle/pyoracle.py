@@ -46,6 +46,16 @@ def _load():
     lib.orc_seal_blocks.restype = ctypes.c_int
     lib.orc_open_blocks.argtypes = [vp, vp, vp, ctypes.c_int64, c_p, c_p]
     lib.orc_open_blocks.restype = ctypes.c_int
+    # vectorised CPU baseline (oracle/xsalsa_simd.c): same secretbox, AVX-512 / AVX2 Salsa20
+    lib.orc_simd_level.restype = ctypes.c_int
+    lib.orc_simd_force.argtypes = [ctypes.c_int]
+    lib.orc_simd_secretbox_seal.argtypes = [vp, vp, ctypes.c_size_t, c_p, c_p]
+    lib.orc_simd_secretbox_open.argtypes = [vp, vp, ctypes.c_size_t, c_p, c_p]
+    lib.orc_simd_secretbox_open.restype = ctypes.c_int
+    lib.orc_simd_seal_blocks.argtypes = [vp, vp, ctypes.c_int64, c_p, c_p]
+    lib.orc_simd_seal_blocks.restype = ctypes.c_int
+    lib.orc_simd_open_blocks.argtypes = [vp, vp, vp, ctypes.c_int64, c_p, c_p]
+    lib.orc_simd_open_blocks.restype = ctypes.c_int
     lib.orc_seal_desc.argtypes = [vp, vp, vp, ctypes.c_int64, c_p]
     lib.orc_seal_desc.restype = ctypes.c_int
     lib.orc_open_desc.argtypes = [vp, vp, vp, vp, ctypes.c_int64, c_p]
