@@ -85,7 +85,12 @@ int xs_seal_object_dev(const uint8_t key[32], const uint8_t nonce0[24], uint64_t
                        void *stream);
 /* Open wire blocks (body_len bytes, block i at i*65552) into d_plain (block i at i*65536).
  * d_ok[i] = 1 if block i authenticated, else 0 and that block's plaintext is zero-filled
- * (secretbox.Open failure, cipher.go:880-893).  Every block must hold > 16 bytes. */
+ * (secretbox.Open failure, cipher.go:880-893).  Every block must hold > 16 bytes.
+ * Unlike x/crypto's Open, which writes nothing on failure, the kernels decrypt and verify in one
+ * pass: a failed block's unauthenticated plaintext is in the destination between its stores and
+ * the zero-fill, both inside the same launch.  Read the destination only after the call's work
+ * has completed (stream-ordered here; the engine calls below return after completion), never
+ * concurrently with it.  This applies to every open entry point of this header. */
 int xs_open_object_dev(const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
                        const void *d_body, uint64_t body_len, void *d_plain, uint8_t *d_ok,
                        void *d_workspace, void *stream);
@@ -138,6 +143,10 @@ xs_engine *xs_engine_create(int device, uint32_t batch_blocks, int nslots);
 void xs_engine_destroy(xs_engine *e);
 int xs_engine_seal(xs_engine *e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
                    const void *plain, uint64_t plain_len, void *body);
+/* xs_engine_open: ok[i] as d_ok above.  With pinned (zero-copy) buffers the kernels write the
+ * plaintext straight into `plain`, so a failed block's bytes transit the caller's buffer before
+ * its zero-fill; the call returns only after both, and `plain` must not be read by another
+ * thread while the call runs. */
 int xs_engine_open(xs_engine *e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
                    const void *body, uint64_t body_len, void *plain, uint8_t *ok);
 /* Seal many host objects and MD5 their crypt files on the GPU -- the hash Fs.put tees off the
