@@ -48,6 +48,9 @@ def parse():
                     help="minimum back-to-back warm-up time: the DVFS clock settles after >= 2 s of load "
                          "(MI355X_MICROARCH.md)")
     ap.add_argument("--blocks", type=int, default=100_000, help="64 KiB blocks per GPU")
+    ap.add_argument("--independent", action="store_true",
+                    help="configs[1] as independent one-block objects, each with its own random nonce "
+                         "(default: the rank's share of one object, nonce0 + block index)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--object-blocks", type=int, default=0,
@@ -556,8 +559,13 @@ def main():
     # this rank's round-robin share of one logical object of world*nb blocks (BASELINE config 4
     # layout); per-block nonces via descriptors, blocks packed contiguously in local HBM
     gidx = shard.owned_blocks(world * nb, world, rank)
-    d_seal = torch.from_numpy(shard.seal_descriptors(nonce0, gidx).view(np.uint8).copy()).to(dev)
-    d_open = torch.from_numpy(shard.seal_descriptors(nonce0, gidx, open_mode=True).view(np.uint8).copy()).to(dev)
+    ds, do = shard.seal_descriptors(nonce0, gidx), shard.seal_descriptors(nonce0, gidx, open_mode=True)
+    if args.independent:  # object g = global block g, nonce from a seeded stream (same for any world size)
+        allnon = np.random.default_rng(0x0B1EC7).integers(0, 256, size=(world * nb, 24), dtype=np.uint8)
+        ds["nonce"] = do["nonce"] = allnon[gidx]
+    block_nonce = [bytes(x) for x in ds["nonce"][[0, 1, nb // 2, nb - 1]]]
+    d_seal = torch.from_numpy(ds.view(np.uint8).copy()).to(dev)
+    d_open = torch.from_numpy(do.view(np.uint8).copy()).to(dev)
     plain = torch.empty(plain_len, dtype=torch.uint8, device=dev)
     device.fill_blocks(plain, rank, world, 0x5EED)  # global block g = rank + world*i, keyed by g
     body = torch.empty(body_len, dtype=torch.uint8, device=dev)
@@ -608,10 +616,10 @@ def main():
         raise SystemExit("bench: round trip failed on rank %d" % rank)
     if rank == 0 and not args.no_cpu:
         from oracle import pyoracle as orc
-        for i in sorted({0, 1, nb // 2, nb - 1}):
+        for j, i in enumerate([0, 1, nb // 2, nb - 1]):
             p = plain[i * BLOCK_DATA:(i + 1) * BLOCK_DATA].cpu().numpy().tobytes()
             w = body[i * BLOCK_SIZE:(i + 1) * BLOCK_SIZE].cpu().numpy().tobytes()
-            if orc.seal(p, orc.nonce_add(nonce0, int(gidx[i])), key) != w:
+            if orc.seal(p, block_nonce[j], key) != w:
                 raise SystemExit("bench: block %d differs from the oracle" % i)
     if world > 1:
         dist.barrier()
@@ -674,9 +682,11 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (SplitMix64 plaintext generated in HBM)",
-            "config": {"workload": f"{nb} x 64KiB device-resident blocks per GPU (round-robin share of "
-                                   f"one {world * nb}-block object), seal then open+verify "
-                                   f"(BASELINE configs[1]+[2] shape)",
+            "config": {"workload": (f"{nb} x 64KiB device-resident one-block objects per GPU, each with its own "
+                                    f"random nonce" if args.independent else
+                                    f"{nb} x 64KiB device-resident blocks per GPU (round-robin share of "
+                                    f"one {world * nb}-block object)") +
+                                   ", seal then open+verify (BASELINE configs[1]+[2] shape)",
                        "blocks_per_gpu": nb, "block_bytes": BLOCK_DATA,
                        "parallelism": f"{world} rank(s), blocks sharded, no data-path collective"},
             "seal_GiB_s": round(nb * BLOCK_DATA / 2**30 / (seal_avg * 1e-3), 3),

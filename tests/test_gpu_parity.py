@@ -144,6 +144,44 @@ def test_full_size_round_trip(dev):
     assert host_plain[0, :4096].cpu().numpy().tobytes() == splitmix64_bytes(0x5EED, 4096)
 
 
+def test_full_size_independent_objects(dev):
+    # config 2's other form: 100k one-block objects, each with its own random
+    # nonce (every 97th about to carry out of byte 7), through descriptor mode; every tag
+    # verified, tampered objects flagged and zero-filled, sampled objects against the oracle
+    from rclone_amd import shard
+    nb = 100_000
+    key = splitmix64_bytes(51, 32)
+    nonces = np.frombuffer(splitmix64_bytes(52, nb * 24), dtype=np.uint8).reshape(nb, 24).copy()
+    nonces[::97, :8] = 0xFF
+    d = np.zeros(nb, dtype=shard.DESC_DTYPE)
+    i = np.arange(nb, dtype=np.uint64)
+    d["src"], d["dst"], d["len"], d["nonce"] = i * 65536, i * 65552, 65536, nonces
+    dopen = d.copy()
+    dopen["src"], dopen["dst"] = i * 65552, i * 65536
+    plain = torch.empty(nb * 65536, dtype=torch.uint8, device="cuda")
+    dev.fill_random(plain, 0x0B1EC7)
+    body = torch.empty(nb * 65552, dtype=torch.uint8, device="cuda")
+    dev.seal_batch(key, d, plain, body)
+    bad = [3, 97 * 5, nb // 2 + 1, nb - 1]
+    tampered = body.clone().view(nb, 65552)
+    for k, b in enumerate(bad):
+        tampered[b, [2, 16, 40000, 65551][k]] ^= 0x21
+    out = torch.empty_like(plain)
+    ok = dev.open_batch(key, dopen, tampered.view(-1), out)
+    okh = ok.cpu().numpy()
+    assert [int(x) for x in np.nonzero(okh == 0)[0]] == bad
+    o2 = out.view(nb, 65536)
+    p2 = plain.view(nb, 65536)
+    good = torch.ones(nb, dtype=torch.bool, device="cuda")
+    good[bad] = False
+    assert bool(torch.equal(o2[good], p2[good]))
+    assert int(o2[~good].sum()) == 0  # zero-filled (pass_bad_blocks contract)
+    hb = body.view(nb, 65552)
+    for b in [0, 1, 97, 65535, nb // 2, nb - 1]:
+        want = orc.seal(p2[b].cpu().numpy().tobytes(), bytes(nonces[b]), key)
+        assert hb[b].cpu().numpy().tobytes() == want, b
+
+
 def test_split_and_wave_paths_agree():
     # batches of <= XS_SPLIT_MAX (256) blocks run four waves per block (xs_seal_split /
     # xs_open_split), larger ones one wave per block: same bytes, tags and verdicts

@@ -1,8 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-for i in 1 2; do
-timeout -k 10 300 python3 bench.py > gpurun_out/bench_r02v_$i.json 2> gpurun_out/bench_r02v_$i.err || { echo BENCH_FAILED; tail -20 gpurun_out/bench_r02v_$i.err; exit 1; }
-python3 -c "
-import json; d=json.loads(open('gpurun_out/bench_r02v_$i.json').read().strip().splitlines()[-1])
-print(d['value'], d['ms_per_step'], d['roofline']['kernel_ms_avg'], d['roofline']['open']['kernel_ms_avg'], d['clock'], d['cpu_baseline'])"
-done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 500 --timeout-method thread -p no:cacheprovider -k "independent or full_size" > gpurun_out/r02x.tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/r02x.tests.log; exit 1; }
+tail -3 gpurun_out/r02x.tests.log
+timeout -k 10 300 python3 bench.py --independent --cpu-seconds 2 > gpurun_out/bench_r02x_indep.json 2> gpurun_out/bench_r02x_indep.err || { echo BENCH_FAILED; tail -20 gpurun_out/bench_r02x_indep.err; exit 1; }
+tail -1 gpurun_out/bench_r02x_indep.json | cut -c1-700
