@@ -713,7 +713,7 @@ static int engine_issue_zero_copy(xs_engine::CSlot& c, const std::vector<uint64_
   if (one_run && nblk <= fused_max_blocks()) {  // tiny batch (a ranged read): one launch
     const bool seal = batch[0]->seal;
     c.seq++;
-    err = launch_crypt_fused(seal, key_arg(batch[0]->key), bounds, dd, nblk, (const uint8_t*)(uintptr_t)sbase,
+    err = launch_crypt_fused(seal, key_arg(batch[0]->key), bounds, dd, c.h_desc, nblk, (const uint8_t*)(uintptr_t)sbase,
                              (uint8_t*)(uintptr_t)dbase, seal ? nullptr : (uint8_t*)(uintptr_t)c.d_h_ok,
                              spin_wait() ? c.d_ctr : nullptr, (uint32_t*)(uintptr_t)c.d_h_flag, c.seq, st);
     c.spin = spin_wait();

@@ -55,10 +55,17 @@ hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const
 // keygen + split crypt in one launch for a tiny descriptor batch under one key (ranged reads);
 // use only when nblocks <= fused_max_blocks().  With ctr != nullptr the last workgroup to finish
 // resets *ctr (device memory, zero before the launch) and stores seq to *flag (pinned host
-// memory, system scope) after every output of the batch is visible to the host.
+// memory, system scope) after every output of the batch is visible to the host.  host_desc
+// (optional): the same descriptors in host memory; batches of <= XS_INLINE_DESCS blocks then travel
+// in the kernel arguments and the kernel does not read desc over PCIe (v2 / v3).
+constexpr int XS_INLINE_DESCS = 16;
+struct XsInlineDescs {
+  xs_block_desc d[XS_INLINE_DESCS];
+  uint32_t n;  // d[0..n) valid; blocks >= n read desc
+};
 hipError_t launch_crypt_fused(bool seal, const KeyArg& key, const NonceArg& bounds, const xs_block_desc* desc,
-                              uint64_t nblocks, const uint8_t* src, uint8_t* dst, uint8_t* ok, uint32_t* ctr,
-                              uint32_t* flag, uint32_t seq, hipStream_t stream);
+                              const xs_block_desc* host_desc, uint64_t nblocks, const uint8_t* src, uint8_t* dst,
+                              uint8_t* ok, uint32_t* ctr, uint32_t* flag, uint32_t seq, hipStream_t stream);
 uint64_t fused_max_blocks();
 hipError_t launch_md5(const xs_md5_desc* d, uint64_t n, const uint8_t* src, uint64_t src_len, uint8_t* digest,
                       uint8_t* ok, hipStream_t stream);

@@ -51,8 +51,8 @@
 #ifndef XS_FUSED_MAX  // single-request descriptor batches up to this many blocks: keygen + crypt in one launch
 #define XS_FUSED_MAX 16
 #endif
-#ifndef XS_FUSED_V  // fused kernel: 1 = keygen then split crypt, 2 = key schedule overlapped with the keystream
-#define XS_FUSED_V 2
+#ifndef XS_FUSED_V  // fused kernel: 1 = keygen then split crypt, 2 / 3 = key schedule overlapped with the
+#define XS_FUSED_V 3  // keystream, four / eight crypt waves
 #endif
 #ifndef XS_KEYGEN_WIDE_MAX  // batches up to this many blocks get one keygen wave per block (latency)
 #define XS_KEYGEN_WIDE_MAX 16
@@ -714,6 +714,31 @@ __device__ __forceinline__ void full_corr_wave(bool seal, uint32_t l, const uint
 // One lane per crypt block.  MODE: 0 object seal, 1 object open, 2 descriptor seal,
 // 3 descriptor open.  Object mode derives nonce, offsets and length from the block
 // index (cipher.go:665-678 nonce.add; :1121 EncryptedSize layout).
+// A descriptor's nonce, offsets and length (MODE 2 seal, 3 open); false when it fails validation
+// (bounds + 16-byte payload alignment).  bounds carries {src_len, dst_len, src base misalignment,
+// dst base misalignment}.
+template <int MODE>
+__device__ __forceinline__ bool desc_params(const xs_block_desc& d, const NonceArg& bounds, uint32_t (&n)[6],
+                                            uint64_t& src, uint64_t& dst, uint32_t& len) {
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    n[i] = (uint32_t)d.nonce[4 * i] | ((uint32_t)d.nonce[4 * i + 1] << 8) | ((uint32_t)d.nonce[4 * i + 2] << 16) |
+           ((uint32_t)d.nonce[4 * i + 3] << 24);
+  }
+  src = d.src_off;
+  dst = d.dst_off;
+  len = d.len;
+  const uint64_t src_len = ((uint64_t)bounds.n[1] << 32) | bounds.n[0];
+  const uint64_t dst_len = ((uint64_t)bounds.n[3] << 32) | bounds.n[2];
+  const uint64_t in_need = (uint64_t)len + (MODE == 3 ? XS_BLOCK_HDR : 0u);
+  const uint64_t out_need = (uint64_t)len + (MODE == 2 ? XS_BLOCK_HDR : 0u);
+  const uint64_t in_pay = src + (MODE == 3 ? XS_BLOCK_HDR : 0u) + bounds.n[4];
+  const uint64_t out_pay = dst + (MODE == 2 ? XS_BLOCK_HDR : 0u) + bounds.n[5];
+  const bool bad = len == 0 || len > XS_BLOCK_DATA || src > src_len || in_need > src_len - src || dst > dst_len ||
+                   out_need > dst_len - dst || (in_pay & 15u) || (out_pay & 15u);
+  return !bad;
+}
+
 // Block b's nonce, offsets and length; false for a descriptor that fails validation.
 template <int MODE>
 __device__ __forceinline__ bool block_params(const NonceArg& nonce0, uint64_t first_block, uint64_t total_len,
@@ -745,26 +770,7 @@ __device__ __forceinline__ bool block_params(const NonceArg& nonce0, uint64_t fi
       len = (uint32_t)(rem < XS_BLOCK_SIZE ? rem : XS_BLOCK_SIZE) - XS_BLOCK_HDR;
     }
   } else {
-    const xs_block_desc& d = desc[b];
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-      n[i] = (uint32_t)d.nonce[4 * i] | ((uint32_t)d.nonce[4 * i + 1] << 8) |
-             ((uint32_t)d.nonce[4 * i + 2] << 16) | ((uint32_t)d.nonce[4 * i + 3] << 24);
-    }
-    src = d.src_off;
-    dst = d.dst_off;
-    len = d.len;
-    // descriptor validation (bounds + 16-byte payload alignment); nonce0 carries
-    // {src_len, dst_len, src base misalignment, dst base misalignment}
-    const uint64_t src_len = ((uint64_t)nonce0.n[1] << 32) | nonce0.n[0];
-    const uint64_t dst_len = ((uint64_t)nonce0.n[3] << 32) | nonce0.n[2];
-    const uint64_t in_need = (uint64_t)len + (MODE == 3 ? XS_BLOCK_HDR : 0u);
-    const uint64_t out_need = (uint64_t)len + (MODE == 2 ? XS_BLOCK_HDR : 0u);
-    const uint64_t in_pay = src + (MODE == 3 ? XS_BLOCK_HDR : 0u) + nonce0.n[4];
-    const uint64_t out_pay = dst + (MODE == 2 ? XS_BLOCK_HDR : 0u) + nonce0.n[5];
-    const bool bad = len == 0 || len > XS_BLOCK_DATA || src > src_len || in_need > src_len - src ||
-                     dst > dst_len || out_need > dst_len - dst || (in_pay & 15u) || (out_pay & 15u);
-    if (bad) return false;
+    return desc_params<MODE>(desc[b], nonce0, n, src, dst, len);
   }
   return true;
 }
@@ -858,12 +864,13 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
 // The body: one wave (lanes l = threadIdx.x & 63) builds block b's key schedule into *o (global
 // memory, or LDS in the fused kernels); pw = 64 x 5 words of LDS scratch private to the wave.
 #ifdef XS_F2_PROBE
-extern __device__ unsigned long long xs_f2_probe[2 * 8 * 16];
+extern __device__ unsigned long long xs_f2_probe[2 * 10 * 16];
 #define KG_MARK(slot)                                                                              \
   do {                                                                                             \
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
     const unsigned long long c_ = __builtin_amdgcn_s_memtime();                                    \
-    if (blockIdx.x == 0 && (threadIdx.x >> 6) == 4 && l < 2u) xs_f2_probe[128 * l + 16 * 5 + (slot)] = l ? c_ : t_; \
+    if (blockIdx.x == 0 && (threadIdx.x >> 6) == (blockDim.x >> 6) - 1u && l < 2u)                   \
+      xs_f2_probe[160 * l + 16 * 9 + (slot)] = l ? c_ : t_;                                          \
   } while (0)
 #else
 #define KG_MARK(slot) \
@@ -871,10 +878,51 @@ extern __device__ unsigned long long xs_f2_probe[2 * 8 * 16];
   } while (0)
 #endif
 
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+// Wait until another wave of the workgroup raised *flag (LDS), then read the 8-word subkey it
+// published at sk (LDS).  Plain LDS reads here would make the compiler first wait for this wave's
+// outstanding LDS-DMA loads (vmcnt), since they could alias: inline ds_reads, lgkmcnt only.
+__device__ __forceinline__ void lds_wait_flag(const uint32_t* flag) {
+  const uint32_t fa = (uint32_t)(uintptr_t)(const lds_u32*)flag;
+  for (;;) {
+    uint32_t f;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(f) : "v"(fa) : "memory");
+    if (__builtin_amdgcn_readfirstlane(f) != 0u) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+// Raise *flag (LDS) once this wave's earlier LDS writes have completed.  Not a release: that would
+// also wait for the wave's outstanding global loads (vmcnt), the PCIe round trip here.
+__device__ __forceinline__ void lds_raise_flag(uint32_t* flag) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_subkey(const uint32_t* flag, const uint32_t* sk, uint32_t out[8]) {
+  const uint32_t ka = (uint32_t)(uintptr_t)(const lds_u32*)sk;
+  lds_wait_flag(flag);
+  uint4 a, b;
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(a), "=&v"(b) : "v"(ka) : "memory");
+  out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
+  out[4] = b.x; out[5] = b.y; out[6] = b.z; out[7] = b.w;
+}
+
+struct KgNoMid {
+  __device__ void operator()() const {}
+};
+template <int MODE, class Mid = KgNoMid>
+__device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32_t n[6], uint64_t src, uint64_t dst,
+                                                 uint32_t len, BlockKey* o, uint32_t (*pw)[5], const uint32_t* sk_lds,
+                                                 const uint32_t* sk_flag, const Mid& mid = Mid());
+
+// sk_lds / sk_flag (LDS, optional): take the HSalsa20 subkey another wave of the workgroup derives
+// for the same block (its LDS writes completed, then *sk_flag raised) instead of computing it
+// again on a shared SIMD.
 template <int MODE>
 __device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& nonce0, uint64_t first_block,
                                             uint64_t total_len, const xs_block_desc* __restrict__ desc,
-                                            uint64_t b, BlockKey* o, uint32_t (*pw)[5]) {
+                                            uint64_t b, BlockKey* o, uint32_t (*pw)[5],
+                                            const uint32_t* sk_lds = nullptr, const uint32_t* sk_flag = nullptr) {
   const uint32_t l = threadIdx.x & 63u;
   uint32_t n[6];
   uint64_t src, dst;
@@ -886,14 +934,31 @@ __device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& n
     }
     return;
   }
-  uint32_t x[16] = {SIG0, key.k[0], key.k[1], key.k[2], key.k[3], SIG1, n[0], n[1],
-                    n[2], n[3],     SIG2,     key.k[4], key.k[5], key.k[6], key.k[7], SIG3};
-#pragma unroll
-  for (int i = 0; i < 16; i++) x[i] = as_varying(x[i]);  // HSalsa20 on the VALU (latency)
+  keygen_wave_body<MODE>(key, n, src, dst, len, o, pw, sk_lds, sk_flag);
+}
+
+// The key schedule of one block whose descriptor fields are already known (and valid).  For a
+// full block, mid() runs once the A and B power tables are in *o (before C, D and the correction
+// term): the fused kernel builds its Toeplitz table there and lets the crypt waves go on.
+template <int MODE, class Mid>
+__device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32_t n[6], uint64_t src, uint64_t dst,
+                                                 uint32_t len, BlockKey* o, uint32_t (*pw)[5], const uint32_t* sk_lds,
+                                                 const uint32_t* sk_flag, const Mid& mid) {
+  const uint32_t l = threadIdx.x & 63u;
+  uint32_t sk[8];
   KG_MARK(0);
-  salsa_rounds_lazy(x);
+  if (sk_lds) {
+    lds_wait_subkey(sk_flag, sk_lds, sk);
+  } else {
+    uint32_t x[16] = {SIG0, key.k[0], key.k[1], key.k[2], key.k[3], SIG1, n[0], n[1],
+                      n[2], n[3],     SIG2,     key.k[4], key.k[5], key.k[6], key.k[7], SIG3};
+#pragma unroll
+    for (int i = 0; i < 16; i++) x[i] = as_varying(x[i]);  // HSalsa20 on the VALU (latency)
+    salsa_rounds_lazy(x);
+    sk[0] = x[0]; sk[1] = x[5]; sk[2] = x[10]; sk[3] = x[15];
+    sk[4] = x[6]; sk[5] = x[7]; sk[6] = x[8]; sk[7] = x[9];
+  }
   KG_MARK(1);
-  uint32_t sk[8] = {x[0], x[5], x[10], x[15], x[6], x[7], x[8], x[9]};
   uint32_t ks[16];
   salsa20_block_lazy(sk, n[4], n[5], l < 32 ? 0u : 1024u, ks);
   KG_MARK(2);
@@ -958,6 +1023,9 @@ __device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& n
     }
     // C[b] = lane b, D[a] = lane 9 + a, A[i] = lane 18 + i, B[j] = lane 27 + j;
     // lane 36: W63 = A[7] B[7] = r^4032, lane 37: r^65 = A[1] C[1], lane 38: r^66 = A[1] C[2]
+    if (l >= 18 && l < 26) put5(o->full.A[l - 18], p);
+    else if (l >= 27 && l < 35) put5(o->full.B[l - 27], p);
+    mid();
     {
       const uint32_t ia = l == 36u ? 25u : 19u, ib = l == 36u ? 34u : l == 37u ? 1u : 2u;
       P5 a, c;
@@ -972,8 +1040,6 @@ __device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& n
     KG_MARK(7);
     if (l < 8) put5(o->full.C[l], p);
     else if (l >= 9 && l < 18) put5(o->full.D[l - 9], p);
-    else if (l >= 18 && l < 26) put5(o->full.A[l - 18], p);
-    else if (l >= 27 && l < 35) put5(o->full.B[l - 27], p);
 #pragma unroll
     for (int i = 0; i < 5; i++) pw[l][i] = p.v[i];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1728,33 +1794,58 @@ __global__ void __launch_bounds__(256) xs_crypt_fused(KeyArg key, NonceArg bound
   }
 }
 
-// Tiny descriptor batches, latency-first (XS_FUSED_V 2, default): one workgroup per block, five
-// waves.  For a full block, waves 0..3 start at once on the data: each stages its four 4 KiB
-// groups with LDS-DMA right after the descriptor read (one PCIe round trip for all of them),
-// computes the HSalsa20 subkey itself and runs its four keystream blocks per lane, writing the
-// output and keeping the ciphertext in LDS; wave 4 meanwhile builds the block's key schedule
-// (keygen_wave: Poly1305 key, power tables, correction term) and the shared Toeplitz digit
-// table, at raised issue priority (it shares wave 0's SIMD, which therefore takes one group and
-// waves 1..3 five each).  After one barrier the four waves run the matrix-core Poly1305 over their LDS-resident
-// ciphertext (phase 2), their accumulators are summed through LDS and wave 0 finalises as
-// crypt_block_mfma does.  The key schedule thus leaves the critical path instead of preceding
-// the whole block.  Partial blocks take the fused-v1 order (keygen, then wave 0's VALU path).
-// Groups per crypt wave: wave 0 also shares its SIMD with the key-schedule wave, so it takes one
-// group and waves 1..3 five each (the key schedule is the longer chain, tools/fused_probe.cpp).
-__device__ __forceinline__ uint32_t f2_first(uint32_t w) { return w == 0u ? 0u : 5u * w - 4u; }
-__device__ __forceinline__ uint32_t f2_count(uint32_t w) { return w == 0u ? 1u : 5u; }
-constexpr int F2_STAGE = 5 * 1024;  // words of staging per crypt wave: up to 5 groups of 4 KiB
-constexpr int F2_LDS_WORDS = 4 * F2_STAGE + 4 * 1024 + 3 * 2048 + 64 * 12;  // stage, relay, acc exchange, Z
+// Tiny descriptor batches, latency-first (XS_FUSED_V 3, default; 2 = the four-crypt-wave form):
+// one workgroup per block.  Descriptors of batches of <= 16 blocks arrive in the kernel arguments.
+// For a full block the crypt waves start at once on the data: each stages its 4 KiB groups with
+// LDS-DMA (one PCIe round trip for all of them), derives the HSalsa20 subkey (or takes it from the
+// wave on its SIMD that did) and runs its keystream blocks, writing the output and keeping the
+// ciphertext in LDS.  The key wave meanwhile builds the block's key schedule (keygen_wave_body,
+// taking wave 0's subkey) at raised issue priority; as soon as the power tables the Toeplitz
+// digit table needs exist it builds that table and raises the Z flag, then finishes C, D and the
+// correction term.  Each crypt wave runs the matrix-core Poly1305 over its own LDS-resident
+// ciphertext once the Z flag is up; after one barrier (B2) their accumulators are summed through
+// LDS and wave 0 finalises as crypt_block_mfma does (the two tail chunks' terms were computed
+// while it waited).  The key schedule thus leaves the critical path.  Cross-wave hand-offs are
+// LDS flags raised after lgkmcnt(0) and polled with inline ds_reads, never release / acquire
+// (those would wait for the waves' outstanding PCIe loads).  Partial blocks take the fused-v1
+// order (key schedule, then wave 0's VALU path).  Phase timings: tools/fused_probe.cpp.
+// NCW crypt waves (4: v2, one per SIMD; 8: v3, two per SIMD so that each SIMD interleaves two
+// dependency chains) plus the key-schedule wave NCW.  Crypt wave w runs on SIMD w % 4; SIMD 0 also
+// runs the key-schedule wave (the longer chain, tools/fused_probe.cpp), so its crypt waves take
+// fewer 4 KiB groups.  Group counts per wave, 4 bits each (wave 0 first), and first groups, 8 bits:
+//   NCW 4: {1, 5, 5, 5}                 -> SIMD loads 1, 5, 5, 5
+//   NCW 8: {1, 3, 3, 3, 0, 2, 2, 2}     -> SIMD loads 1, 5, 5, 5 (wave 4 idles until phase 2)
+// With NCW 8, waves 4..7 take the HSalsa20 subkey from wave w - 4 (same SIMD) through LDS instead
+// of computing it again: a SIMD's second wave only gets the issue slots its first leaves.
+#ifndef XS_F3_DIST  // NCW 8 group split: 0 = {1, 3, 3, 3, 0, 2, 2, 2}; 1 = two groups per crypt wave
+#define XS_F3_DIST 0
+#endif
+template <int NCW>
+__device__ __forceinline__ uint32_t f2_count(uint32_t w) {
+  constexpr uint32_t c = NCW == 4 ? 0x5551u : XS_F3_DIST ? 0x22222222u : 0x22203331u;
+  return (c >> (4u * w)) & 15u;
+}
+template <int NCW>
+__device__ __forceinline__ uint32_t f2_first(uint32_t w) {
+  constexpr uint64_t f = NCW == 4 ? 0x0B060100ull : XS_F3_DIST ? 0x0E0C0A0806040200ull : 0x0E0C0A0A07040100ull;
+  return (uint32_t)(f >> (8u * w)) & 255u;
+}
+template <int NCW>
+constexpr int f2_max_groups() { return NCW == 4 ? 5 : XS_F3_DIST ? 2 : 3; }
+// LDS words: stage (16 groups of 4 KiB, indexed by group), relay (4 KiB per crypt wave), the
+// accumulators of crypt waves 1..NCW-1 (8 KiB each), the Toeplitz digit rows (3 KiB)
+template <int NCW>
+constexpr int f2_lds_words() { return 16 * 1024 + NCW * 1024 + (NCW - 1) * 2048 + 64 * 12; }
 
 #ifdef XS_F2_PROBE
 // Diagnostic build only (tools/fused_probe.cpp): s_memrealtime (100 MHz) at phase boundaries, per
 // wave of workgroup 0, lane-indexed vector stores.
-__device__ unsigned long long xs_f2_probe[2 * 8 * 16];
+__device__ unsigned long long xs_f2_probe[2 * 10 * 16];  // [clock][wave 0..9][slot]; row 9: keygen_wave
 #define F2_MARK(slot)                                                                        \
   do {                                                                                       \
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                          \
     const unsigned long long c_ = __builtin_amdgcn_s_memtime();                              \
-    if (blockIdx.x == 0 && l < 2u) xs_f2_probe[128 * l + 16 * wave + (slot)] = l ? c_ : t_;   \
+    if (blockIdx.x == 0 && l < 2u) xs_f2_probe[160 * l + 16 * wave + (slot)] = l ? c_ : t_;   \
   } while (0)
 #else
 #define F2_MARK(slot) \
@@ -1762,24 +1853,31 @@ __device__ unsigned long long xs_f2_probe[2 * 8 * 16];
   } while (0)
 #endif
 
-template <bool SEAL>
-__global__ void __launch_bounds__(320) xs_crypt_fused2(KeyArg key, NonceArg bounds, const xs_block_desc* __restrict__ desc,
+template <bool SEAL, int NCW>
+__global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, NonceArg bounds, const xs_block_desc* __restrict__ desc,
+                                                                    const XsInlineDescs inl,
                                                        uint64_t nblocks, const uint8_t* __restrict__ src,
                                                        uint8_t* __restrict__ dst, uint8_t* __restrict__ ok,
                                                        uint32_t* __restrict__ ctr, uint32_t* __restrict__ flag,
                                                        uint32_t seq) {
   constexpr int MODE = SEAL ? 2 : 3;
-  __shared__ __attribute__((aligned(16))) uint32_t lds[F2_LDS_WORDS];
+  static_assert(f2_lds_words<NCW>() >= LDS_WORDS, "the fallback path runs crypt_wave in this LDS");
+  __shared__ __attribute__((aligned(16))) uint32_t lds[f2_lds_words<NCW>()];
   __shared__ BlockKey kl;
   __shared__ uint32_t pw[64][5];
+  // hs_flag[0..3]: subkeys of waves 0..3 published (for waves 4..7 / the key wave); [4]: Z table ready
+  __shared__ uint32_t hs_key[4][8], hs_flag[5];
   if (blockIdx.x >= nblocks) return;  // uniform per workgroup (grid == nblocks)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63u;
   const uint64_t blk = blockIdx.x;
+  if (threadIdx.x < 5u) hs_flag[threadIdx.x] = 0u;
   F2_MARK(0);
   uint32_t nn[6];
   uint64_t soff, doff;
   uint32_t len;
-  const bool valid = block_params<MODE>(bounds, 0, 0, desc, blk, nn, soff, doff, len);
+  // descriptors of small batches come in the kernel arguments (no PCIe read of the pinned array)
+  const bool valid = blk < inl.n ? desc_params<MODE>(inl.d[blk], bounds, nn, soff, doff, len)
+                                : block_params<MODE>(bounds, 0, 0, desc, blk, nn, soff, doff, len);
   // The descriptor is uniform: move it into SGPRs now.  vmcnt drains in order, so a later use of
   // a descriptor word still in a VGPR would make the compiler wait for every data load of the
   // block issued after it.
@@ -1792,17 +1890,25 @@ __global__ void __launch_bounds__(320) xs_crypt_fused2(KeyArg key, NonceArg boun
   doff = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(doff >> 32)) << 32) |
          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)doff);
   len = __builtin_amdgcn_readfirstlane(len);
+  __syncthreads();  // hs_flag cleared before any wave can poll or raise it
   F2_MARK(1);
   if (!valid || len != XS_BLOCK_DATA) {
-    // rejected descriptor or partial block: the fused-v1 order (wave 4 idles)
-    if (wave == 0) keygen_wave<MODE>(key, bounds, 0, 0, desc, blk, &kl, pw);
+    // rejected descriptor or partial block: the fused-v1 order (the other waves idle)
+    if (wave == 0) {
+      if (valid) {
+        keygen_wave_body<MODE>(key, nn, soff, doff, len, &kl, pw, nullptr, nullptr);
+      } else if (l == 0u) {
+        kl.flags = 1;
+        kl.len = 0;
+      }
+    }
     __syncthreads();
     if (wave < 4) crypt_wave<SEAL, 4, true>(&kl, nblocks, src, dst, ok, lds);
   } else {
-    uint32_t* const stage = lds;                      // [4][4096]
-    uint32_t* const relay = lds + 4 * F2_STAGE;       // [4][1024]: OPEN output relayout; wave 0's transpose
-    uint32_t* const xacc = relay + 4 * 1024;          // [3][2048]: accumulators of waves 1..3
-    uint32_t* const zt = xacc + 3 * 2048;             // [64][12]: Toeplitz digit rows
+    uint32_t* const stage = lds;                      // [16][1024]: group u at 1024 u
+    uint32_t* const relay = lds + 16 * 1024;          // [NCW][1024]: OPEN output relayout; wave 0's transpose
+    uint32_t* const xacc = relay + NCW * 1024;        // [NCW - 1][2048]: accumulators of waves 1..NCW-1
+    uint32_t* const zt = xacc + (NCW - 1) * 2048;     // [64][12]: Toeplitz digit rows
     const uint8_t* in = src + soff;
     uint8_t* out = dst + doff;
     const uint8_t* pin = SEAL ? in : in + XS_BLOCK_HDR;
@@ -1813,23 +1919,22 @@ __global__ void __launch_bounds__(320) xs_crypt_fused2(KeyArg key, NonceArg boun
     const bool not_key = (l & 47u) != 0u;
     const uint32_t n = l & 15u, kg = l >> 4;
     uint4 tail[2];  // wave 0 lane 63: chunks 4094, 4095 (fetched early, used in the finalisation)
-    if (wave < 4) {
-      // ---- phase 1: stage all four groups, keystream + XOR + output, ciphertext kept in LDS
-      uint32_t* const sw = stage + F2_STAGE * wave;
+    if (wave < NCW) {
+      // ---- phase 1: stage all this wave's groups, keystream + XOR + output, ciphertext kept in LDS
       if (wave == 0 && l == 0u) {  // key slots (chunks -2, -1): never loaded or stored
-        *reinterpret_cast<uint4*>(sw) = make_uint4(0u, 0u, 0u, 0u);
-        *reinterpret_cast<uint4*>(sw + 64) = make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(stage) = make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(stage + 64) = make_uint4(0u, 0u, 0u, 0u);
       }
-      const uint32_t g0 = f2_first(wave), gn = f2_count(wave);
+      const uint32_t g0 = f2_first<NCW>(wave), gn = f2_count<NCW>(wave);
 #pragma unroll
-      for (uint32_t g = 0; g < 5; g++) {
+      for (uint32_t g = 0; g < (uint32_t)f2_max_groups<NCW>(); g++) {
         if (g >= gn) break;
         const uint32_t u = g0 + g;
 #pragma unroll
         for (int j = 0; j < 4; j++)
           if (j > 0 || u > 0 || not_key)
             __builtin_amdgcn_global_load_lds(pin_m32 + 4096u * u + lane_off + 1024 * j,
-                                             (lds_void*)(sw + 1024 * g + 256 * j), 16, 0, 0);
+                                             (lds_void*)(stage + 1024 * u + 256 * j), 16, 0, 0);
       }
       if (wave == 0) {  // every lane loads the same two chunks (lane 63 uses them); a lane-varying
                         // zero keeps them VGPR loads that nothing waits for before the finalisation
@@ -1838,13 +1943,24 @@ __global__ void __launch_bounds__(320) xs_crypt_fused2(KeyArg key, NonceArg boun
         tail[1] = *reinterpret_cast<const uint4*>(tp + 16);
       }
       F2_MARK(14);
-      uint32_t x[16] = {SIG0, key.k[0], key.k[1], key.k[2], key.k[3], SIG1, nn[0], nn[1],
-                        nn[2], nn[3],     SIG2,     key.k[4], key.k[5], key.k[6], key.k[7], SIG3};
+      uint32_t sk[8];
+      if (NCW == 8 && wave >= 4u) {  // the subkey of wave - 4, which shares this SIMD
+        if (gn != 0u) lds_wait_subkey(&hs_flag[wave - 4u], hs_key[wave - 4u], sk);
+      } else {
+        uint32_t x[16] = {SIG0, key.k[0], key.k[1], key.k[2], key.k[3], SIG1, nn[0], nn[1],
+                          nn[2], nn[3],     SIG2,     key.k[4], key.k[5], key.k[6], key.k[7], SIG3};
 #pragma unroll
-      for (int i = 0; i < 16; i++) x[i] = as_varying(x[i]);  // on the VALU: see as_varying
-      salsa_rounds_lazy(x);  // HSalsa20 (each crypt wave derives the subkey itself: no wait on wave 4)
+        for (int i = 0; i < 16; i++) x[i] = as_varying(x[i]);  // on the VALU: see as_varying
+        salsa_rounds_lazy(x);  // HSalsa20 (the crypt waves derive the subkey themselves: no wait on the key wave)
+        sk[0] = x[0]; sk[1] = x[5]; sk[2] = x[10]; sk[3] = x[15];
+        sk[4] = x[6]; sk[5] = x[7]; sk[6] = x[8]; sk[7] = x[9];
+        if (l == 0u) {
+#pragma unroll
+          for (int i = 0; i < 8; i++) hs_key[wave][i] = sk[i];
+        }
+        lds_raise_flag(&hs_flag[wave]);
+      }
       F2_MARK(15);
-      const uint32_t sk[8] = {x[0], x[5], x[10], x[15], x[6], x[7], x[8], x[9]};
       const SalsaPre pre = salsa_pre(sk, nn[4], nn[5]);
       F2_MARK(2);
       uint32_t* const rl = relay + 1024 * wave;
@@ -1856,7 +1972,7 @@ __global__ void __launch_bounds__(320) xs_crypt_fused2(KeyArg key, NonceArg boun
         F2_MARK(3 + 2 * g);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         F2_MARK(4 + 2 * g);
-        uint32_t* sb = sw + 1024 * g;
+        uint32_t* sb = stage + 1024 * u;
         uint4* mine = reinterpret_cast<uint4*>(sb + 256 * (l >> 4) + 4 * (l & 15u));
         uint32_t o[16];
 #pragma unroll
@@ -1885,43 +2001,70 @@ __global__ void __launch_bounds__(320) xs_crypt_fused2(KeyArg key, NonceArg boun
       if (!SEAL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // plaintext out before any zero-fill
       F2_MARK(11);
     } else {
-      // ---- wave 4: key schedule into LDS, then the shared Toeplitz digit table.  It shares a
-      // SIMD with wave 0 and is the longer chain: it issues first.
+      // ---- the key wave: key schedule into LDS; as soon as the A and B power tables exist, the
+      // shared Toeplitz digit table and the Z-ready flag (the crypt waves' MFMA phase needs no
+      // more), then C, D and the correction term, which only the finalisation reads (after B2).
+      // It shares a SIMD with wave 0 and is the longer chain: it issues first.
       __builtin_amdgcn_s_setprio(3);
-      keygen_wave<MODE>(key, bounds, 0, 0, desc, blk, &kl, pw);
-      F2_MARK(2);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      P5 qa, qb;
-      const uint32_t k = 63u - l;
+      auto z_table = [&]() {
+        F2_MARK(2);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        P5 qa, qb;
+        const uint32_t k = 63u - l;
 #pragma unroll
-      for (int i = 0; i < 5; i++) {
-        qa.v[i] = kl.full.A[k & 7u][i];
-        qb.v[i] = kl.full.B[k >> 3][i];
-      }
-      const P32 wq = to32(pmul(qa, qb));
-      uint32_t w0 = wq.w0, w1 = wq.w1, w2 = wq.w2, w3 = wq.w3, w4 = wq.w4;
-      unsigned cy;
-      w0 = __builtin_addc(w0, 0x80808080u, 0u, &cy);
-      w1 = __builtin_addc(w1, 0x80808080u, cy, &cy);
-      w2 = __builtin_addc(w2, 0x80808080u, cy, &cy);
-      w3 = __builtin_addc(w3, 0x80808080u, cy, &cy);
-      w4 = (w4 + 0x80u + cy) ^ 0x80u;
-      w0 ^= 0x80808080u;
-      w1 ^= 0x80808080u;
-      w2 ^= 0x80808080u;
-      w3 ^= 0x80808080u;
-      uint4* row = reinterpret_cast<uint4*>(zt + 12u * l);
-      row[0] = make_uint4(0u, 0u, 0u, w4 << 24);
-      row[1] = make_uint4(__builtin_bswap32(w3), __builtin_bswap32(w2), __builtin_bswap32(w1), __builtin_bswap32(w0));
-      row[2] = make_uint4(0u, 0u, 0u, 0u);
-      F2_MARK(3);
+        for (int i = 0; i < 5; i++) {
+          qa.v[i] = kl.full.A[k & 7u][i];
+          qb.v[i] = kl.full.B[k >> 3][i];
+        }
+        const P32 wq = to32(pmul(qa, qb));
+        uint32_t w0 = wq.w0, w1 = wq.w1, w2 = wq.w2, w3 = wq.w3, w4 = wq.w4;
+        unsigned cy;
+        w0 = __builtin_addc(w0, 0x80808080u, 0u, &cy);
+        w1 = __builtin_addc(w1, 0x80808080u, cy, &cy);
+        w2 = __builtin_addc(w2, 0x80808080u, cy, &cy);
+        w3 = __builtin_addc(w3, 0x80808080u, cy, &cy);
+        w4 = (w4 + 0x80u + cy) ^ 0x80u;
+        w0 ^= 0x80808080u;
+        w1 ^= 0x80808080u;
+        w2 ^= 0x80808080u;
+        w3 ^= 0x80808080u;
+        uint4* row = reinterpret_cast<uint4*>(zt + 12u * l);
+        row[0] = make_uint4(0u, 0u, 0u, w4 << 24);
+        row[1] = make_uint4(__builtin_bswap32(w3), __builtin_bswap32(w2), __builtin_bswap32(w1), __builtin_bswap32(w0));
+        row[2] = make_uint4(0u, 0u, 0u, 0u);
+        lds_raise_flag(&hs_flag[4]);
+        F2_MARK(3);
+      };
+      // the descriptor fields this kernel already holds (no second read over PCIe); wave 0's subkey
+      keygen_wave_body<MODE>(key, nn, soff, doff, len, &kl, pw, hs_key[0], &hs_flag[0], z_table);
     }
-    __syncthreads();  // B1: key schedule, Z table and every wave's staged ciphertext are in LDS
-    F2_MARK(12);
     xs_v4i acc[4][2];
-    if (wave < 4) {
+    P5 tl;  // wave 0, lane 63: the Poly1305 terms of chunks 4094, 4095
+#pragma unroll
+    for (int i = 0; i < 5; i++) tl.v[i] = 0;
+    if (wave < NCW) {
+      lds_wait_flag(&hs_flag[4]);  // the Z table (each wave reads only its own staged groups)
+      F2_MARK(12);
+      if (wave == 0 && l == 63u) {
+        // chunks 4094, 4095 (keystream block 1024 words 0..7): exponents 2 and 1.  r and ks1024
+        // are in kl before the Z flag rises, so this leaves the finalisation's critical path.
+        P5 rr;
+#pragma unroll
+        for (int i = 0; i < 5; i++) rr.v[i] = kl.r[i];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          const uint32_t w[4] = {tail[j].x, tail[j].y, tail[j].z, tail[j].w};
+          uint32_t o4[4];
+#pragma unroll
+          for (int i = 0; i < 4; i++) o4[i] = w[i] ^ kl.ks1024[4 * j + i];
+          *reinterpret_cast<uint4*>(pout + 16u * (4094u + j)) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+          const uint32_t* cw = SEAL ? o4 : w;
+          padd_full(tl, cw[0], cw[1], cw[2], cw[3]);
+          tl = pmul(tl, rr);
+        }
+      }
       // ---- phase 2: matrix-core Poly1305 over the LDS-resident ciphertext
       const uint32_t zlo = (15u - n) >> 2, zsh = (31u - n) & 3u;
       uint32_t zaddr = (uint32_t)(uintptr_t)((const lds_u32*)zt + 12u * kg + zlo);
@@ -1933,12 +2076,11 @@ __global__ void __launch_bounds__(320) xs_crypt_fused2(KeyArg key, NonceArg boun
         for (int mt = 0; mt < 2; mt++)
 #pragma unroll
           for (int i = 0; i < 4; i++) acc[j][mt][i] = wave == 0 ? 1 << 24 : 0;  // the bias once per block
-      const uint32_t* sw = stage + F2_STAGE * wave;
-      const uint32_t g0 = f2_first(wave), gn = f2_count(wave);
+      const uint32_t g0 = f2_first<NCW>(wave), gn = f2_count<NCW>(wave);
 #pragma unroll 1
       for (uint32_t g = 0; g < gn; g++) {
         const uint32_t u = g0 + g;
-        const uint4* mine = reinterpret_cast<const uint4*>(sw + 1024 * g + 256 * (l >> 4) + 4 * (l & 15u));
+        const uint4* mine = reinterpret_cast<const uint4*>(stage + 1024 * u + 256 * (l >> 4) + 4 * (l & 15u));
         uint32_t cw[16];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -1965,25 +2107,24 @@ __global__ void __launch_bounds__(320) xs_crypt_fused2(KeyArg key, NonceArg boun
         }
       }
       if (wave > 0) {
+        // lane-contiguous 16-byte groups: conflict-free ds_write_b128 / ds_read_b128
 #pragma unroll
         for (int j = 0; j < 4; j++)
 #pragma unroll
           for (int mt = 0; mt < 2; mt++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) xacc[(wave - 1u) * 2048u + (uint32_t)(8 * j + 4 * mt + i) * 64u + l] = acc[j][mt][i];
+            *reinterpret_cast<xs_v4i*>(xacc + (wave - 1u) * 2048u + (uint32_t)(2 * j + mt) * 256u + 4u * l) = acc[j][mt];
       }
     }
     __syncthreads();  // B2: the other waves' accumulators are in LDS
     F2_MARK(13);
     if (wave == 0) {
 #pragma unroll
-      for (int w = 0; w < 3; w++)
+      for (int w = 0; w < NCW - 1; w++)
 #pragma unroll
         for (int j = 0; j < 4; j++)
 #pragma unroll
           for (int mt = 0; mt < 2; mt++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) acc[j][mt][i] += (int)xacc[(uint32_t)w * 2048u + (uint32_t)(8 * j + 4 * mt + i) * 64u + l];
+            acc[j][mt] += *reinterpret_cast<const xs_v4i*>(xacc + (uint32_t)w * 2048u + (uint32_t)(2 * j + mt) * 256u + 4u * l);
       // transpose the partial words through wave 0's relay slot (as crypt_block_mfma)
       uint64_t* t64 = reinterpret_cast<uint64_t*>(relay);
 #pragma unroll
@@ -2023,24 +2164,7 @@ __global__ void __launch_bounds__(320) xs_crypt_fused2(KeyArg key, NonceArg boun
 #pragma unroll
         for (int i = 0; i < 5; i++) hs.v[i] += bk->corr[i];
       }
-      if (l == 63u) {  // chunks 4094, 4095 (keystream block 1024 words 0..7): exponents 2 and 1
-        P5 rr, tl;
-#pragma unroll
-        for (int i = 0; i < 5; i++) {
-          rr.v[i] = bk->r[i];
-          tl.v[i] = 0;
-        }
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-          const uint32_t w[4] = {tail[j].x, tail[j].y, tail[j].z, tail[j].w};
-          uint32_t o4[4];
-#pragma unroll
-          for (int i = 0; i < 4; i++) o4[i] = w[i] ^ bk->ks1024[4 * j + i];
-          *reinterpret_cast<uint4*>(pout + 16u * (4094u + j)) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
-          const uint32_t* cw = SEAL ? o4 : w;
-          padd_full(tl, cw[0], cw[1], cw[2], cw[3]);
-          tl = pmul(tl, rr);
-        }
+      if (l == 63u) {  // chunks 4094, 4095, computed before B2
 #pragma unroll
         for (int i = 0; i < 5; i++) hs.v[i] += tl.v[i];
       }
@@ -2177,16 +2301,26 @@ hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const
 }
 
 hipError_t launch_crypt_fused(bool seal, const KeyArg& key, const NonceArg& bounds, const xs_block_desc* desc,
-                              uint64_t nblocks, const uint8_t* src, uint8_t* dst, uint8_t* ok, uint32_t* ctr,
-                              uint32_t* flag, uint32_t seq, hipStream_t stream) {
+                              const xs_block_desc* host_desc, uint64_t nblocks, const uint8_t* src, uint8_t* dst,
+                              uint8_t* ok, uint32_t* ctr, uint32_t* flag, uint32_t seq, hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
-  static const int version = [] {  // env XS_FUSED_V: 1 = keygen then split crypt, 2 = overlapped (A/B)
+  XsInlineDescs inl{};
+  if (host_desc && nblocks <= (uint64_t)XS_INLINE_DESCS) {
+    for (uint64_t i = 0; i < nblocks; i++) inl.d[i] = host_desc[i];
+    inl.n = (uint32_t)nblocks;
+  }
+  static const int version = [] {  // env XS_FUSED_V: 1 = keygen then split crypt, 2 / 3 = overlapped (A/B)
     const char* v = getenv("XS_FUSED_V");
     return v ? atoi(v) : XS_FUSED_V;
   }();
-  if (version >= 2) {
-    if (seal) hipLaunchKernelGGL(xs_crypt_fused2<true>, dim3((unsigned)nblocks), dim3(320), 0, stream, key, bounds, desc, nblocks, src, dst, ok, ctr, flag, seq);
-    else hipLaunchKernelGGL(xs_crypt_fused2<false>, dim3((unsigned)nblocks), dim3(320), 0, stream, key, bounds, desc, nblocks, src, dst, ok, ctr, flag, seq);
+  if (version >= 3) {  // eight crypt waves (two per SIMD) + the key-schedule wave
+    if (seal) hipLaunchKernelGGL((xs_crypt_fused2<true, 8>), dim3((unsigned)nblocks), dim3(576), 0, stream, key, bounds, desc, inl, nblocks, src, dst, ok, ctr, flag, seq);
+    else hipLaunchKernelGGL((xs_crypt_fused2<false, 8>), dim3((unsigned)nblocks), dim3(576), 0, stream, key, bounds, desc, inl, nblocks, src, dst, ok, ctr, flag, seq);
+    return hipGetLastError();
+  }
+  if (version == 2) {  // four crypt waves (one per SIMD) + the key-schedule wave
+    if (seal) hipLaunchKernelGGL((xs_crypt_fused2<true, 4>), dim3((unsigned)nblocks), dim3(320), 0, stream, key, bounds, desc, inl, nblocks, src, dst, ok, ctr, flag, seq);
+    else hipLaunchKernelGGL((xs_crypt_fused2<false, 4>), dim3((unsigned)nblocks), dim3(320), 0, stream, key, bounds, desc, inl, nblocks, src, dst, ok, ctr, flag, seq);
     return hipGetLastError();
   }
   if (seal) hipLaunchKernelGGL(xs_crypt_fused<true>, dim3((unsigned)nblocks), dim3(256), 0, stream, key, bounds, desc, nblocks, src, dst, ok, ctr, flag, seq);

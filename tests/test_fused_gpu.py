@@ -158,8 +158,9 @@ def _run(version):
 def test_fused_versions_agree_with_oracle():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    v1, v2 = _run(1), _run(2)
-    assert v1["bad"] == [] and v2["bad"] == [], (v1["nbad"], v1["bad"], v2["nbad"], v2["bad"])
+    v1, v2, v3 = _run(1), _run(2), _run(3)
+    for v in (v1, v2, v3):
+        assert v["bad"] == [], (v["nbad"], v["bad"])
     assert v2["concurrent"]["batches"] < v2["concurrent"]["requests"]  # the concurrent opens did coalesce
-    assert v1["cases"] == v2["cases"] > 150
-    assert v1["digest"] == v2["digest"]
+    assert v1["cases"] == v2["cases"] == v3["cases"] > 150
+    assert v1["digest"] == v2["digest"] == v3["digest"]

@@ -1,6 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 500 --timeout-method thread -p no:cacheprovider -k "independent or full_size" > gpurun_out/r02x.tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/r02x.tests.log; exit 1; }
-tail -3 gpurun_out/r02x.tests.log
-timeout -k 10 300 python3 bench.py --independent --cpu-seconds 2 > gpurun_out/bench_r02x_indep.json 2> gpurun_out/bench_r02x_indep.err || { echo BENCH_FAILED; tail -20 gpurun_out/bench_r02x_indep.err; exit 1; }
-tail -1 gpurun_out/bench_r02x_indep.json | cut -c1-700
+rm -rf gpurun_out/fv_* gpurun_out/fvprof_*
+timeout -k 10 900 python -u -m pytest -x -q --timeout 500 --timeout-method thread -p no:cacheprovider tests/test_fused_gpu.py tests/test_gpu_parity.py tests/test_engine_coalesce_gpu.py tests/test_cipher_gpu.py > gpurun_out/r02ah.tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/r02ah.tests.log; exit 1; }
+tail -2 gpurun_out/r02ah.tests.log
+bash tools/fused_v_ab.sh > gpurun_out/fv_ab.log 2>&1 || { echo AB_FAILED; tail -20 gpurun_out/fv_ab.log; exit 1; }
+for f in gpurun_out/fv_seek_*.json; do echo $f $(python3 -c "import json; d=json.load(open('$f')); print(d['p50_us'], d['p90_us'], d['p99_us'], d['reads_per_s'], d['bad'])"); done
