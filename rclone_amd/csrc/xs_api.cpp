@@ -14,8 +14,10 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -33,6 +35,49 @@ void set_error(const char* fmt, ...) {
   vsnprintf(buf, sizeof buf, fmt, ap);
   va_end(ap);
   g_err = buf;
+}
+}  // namespace xs
+
+// Pinned allocations made by xs_host_alloc (portable: mapped for every device): base -> (size,
+// device address).  Engine requests on such buffers (every rc_* handle's staging) resolve their
+// device address here instead of two HIP pointer queries per buffer per request.
+namespace xs {
+struct PinRange {
+  size_t size;
+  uint64_t dev;
+};
+static std::shared_mutex& pin_mu() {
+  static std::shared_mutex* m = new std::shared_mutex();  // leaked: used until process exit
+  return *m;
+}
+static std::map<uintptr_t, PinRange>& pins() {
+  static auto* m = new std::map<uintptr_t, PinRange>();
+  return *m;
+}
+void pin_register(void* p, size_t size) {
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || !d) {
+    (void)hipGetLastError();
+    return;  // not resolvable up front: such requests take the HIP query path
+  }
+  std::unique_lock<std::shared_mutex> g(pin_mu());
+  pins()[(uintptr_t)p] = PinRange{size, (uint64_t)(uintptr_t)d};
+}
+void pin_unregister(void* p) {
+  std::unique_lock<std::shared_mutex> g(pin_mu());
+  pins().erase((uintptr_t)p);
+}
+// Device address of p when it lies inside a registered allocation.
+static bool pin_lookup(const void* p, uint64_t* dev) {
+  std::shared_lock<std::shared_mutex> g(pin_mu());
+  auto& m = pins();
+  auto it = m.upper_bound((uintptr_t)p);
+  if (it == m.begin()) return false;
+  --it;
+  const uintptr_t off = (uintptr_t)p - it->first;
+  if (off >= it->second.size) return false;
+  *dev = it->second.dev + off;
+  return true;
 }
 }  // namespace xs
 
@@ -254,11 +299,14 @@ void* xs_host_alloc(size_t bytes) {
     set_error("hipHostMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
     return nullptr;
   }
+  xs::pin_register(p, bytes ? bytes : 1);
   return p;
 }
 
 void xs_host_free(void* p) {
-  if (p) (void)hipHostFree(p);
+  if (!p) return;
+  xs::pin_unregister(p);
+  (void)hipHostFree(p);
 }
 
 }  // extern "C"
@@ -348,6 +396,7 @@ struct xs_engine {
 // (pageable memory, device memory): only such buffers are handed to the kernels directly.
 static bool host_dev_ptr(const void* p, uint64_t* dev, int device) {
   if (!p) return false;
+  if (pin_lookup(p, dev)) return true;  // xs_host_alloc memory: portable, mapped for every device
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();  // pageable memory reports an error; clear it

@@ -164,3 +164,48 @@ def test_fused_versions_agree_with_oracle():
     assert v2["concurrent"]["batches"] < v2["concurrent"]["requests"]  # the concurrent opens did coalesce
     assert v1["cases"] == v2["cases"] == v3["cases"] > 150
     assert v1["digest"] == v2["digest"] == v3["digest"]
+
+
+def test_first_fused_open_on_fresh_engines_reports_tampering():
+    # the pinned completion word must start cleared on every new engine, or the first
+    # fused batch could be taken as done before its kernel ran (stale verdicts).  Engines are
+    # created and destroyed repeatedly (pinned memory is recycled between them, after being
+    # filled with the first sequence number), and the very first operation on each is a
+    # tampered one-block open.
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import ctypes
+
+    from oracle import pyoracle as orc
+    from rclone_amd import _lib
+    from rclone_amd.testdata import splitmix64_bytes
+    L = _lib.lib()
+    key, nonce = splitmix64_bytes(81, 32), splitmix64_bytes(82, 24)
+    plain = splitmix64_bytes(83, 65536)
+    good = orc.seal(plain, nonce, key)
+    bad = bytearray(good)
+    bad[5] ^= 0x40  # the tag
+    win = L.xs_host_alloc(len(good))
+    out = L.xs_host_alloc(65536)
+    try:
+        for rep in range(6):
+            junk = L.xs_host_alloc(1 << 16)  # recycled pinned memory holding the value 1
+            ctypes.memset(junk, 1, 1 << 16)
+            L.xs_host_free(junk)
+            e = L.xs_engine_create(0, 64, 3)
+            assert e
+            try:
+                ok = (ctypes.c_uint8 * 1)(1)
+                ctypes.memmove(win, bytes(bad), len(bad))
+                ctypes.memset(out, 0x5A, 65536)
+                assert L.xs_engine_open(e, key, nonce, 0, win, len(bad), out, ok) == 0
+                assert ok[0] == 0, rep
+                assert ctypes.string_at(out, 65536) == bytes(65536), rep  # zero-filled
+                ctypes.memmove(win, good, len(good))
+                assert L.xs_engine_open(e, key, nonce, 0, win, len(good), out, ok) == 0
+                assert ok[0] == 1 and ctypes.string_at(out, 65536) == plain, rep
+            finally:
+                L.xs_engine_destroy(e)
+    finally:
+        L.xs_host_free(win)
+        L.xs_host_free(out)
