@@ -342,13 +342,20 @@ struct xs_engine {
     bool zc;
     uint64_t d_in, d_out;
     uint64_t blk0;  // first block within its combined batch
+    // woken (under qmu) when the request is done or when it heads the queue and the lead is free:
+    // one waiter at a time, not every caller on each completion
+    std::condition_variable cv;
   };
   bool coalesce = true;
   int host_md5_threads = -1;  // -1: the default (XS_MD5_HOST_THREADS or half the cores, <= 8); 0: GPU only
   bool zero_copy = true;  // pinned caller buffers go to the kernels directly (no staging copies)
   std::mutex qmu;
-  std::condition_variable qcv;
   std::vector<Req*> queue;
+  std::atomic<size_t> qcount{0};  // queue.size(), readable without qmu (the leader's issue-while-waiting poll)
+  bool overlap = false;           // XS_ENGINE_OVERLAP=1: the leader issues newly queued requests while it
+                                  // waits (lower latency at low load, less coalescing: off by default)
+  bool wake_all = false;          // XS_ENGINE_WAKE_ALL=1: one shared condition, every waiter woken (A/B)
+  std::condition_variable qcv;    // the shared condition of wake_all
   bool leader = false;
   struct CSlot {  // one combined batch in flight
     hipStream_t s = nullptr;
@@ -548,6 +555,8 @@ extern "C" xs_engine* xs_engine_create(int device, uint32_t batch_blocks, int ns
   if (const char* v = getenv("XS_ENGINE_COALESCE")) e->coalesce = atoi(v) != 0;
   if (const char* v = getenv("XS_ENGINE_ZERO_COPY")) e->zero_copy = atoi(v) != 0;
   if (const char* v = getenv("XS_EXPRESS_MAX")) e->express_max = strtoull(v, nullptr, 10);
+  if (const char* v = getenv("XS_ENGINE_OVERLAP")) e->overlap = atoi(v) != 0;
+  if (const char* v = getenv("XS_ENGINE_WAKE_ALL")) e->wake_all = atoi(v) != 0;
   return e;
 }
 
@@ -728,6 +737,16 @@ static NonceArg bounds_arg(uint64_t src_len, uint64_t dst_len);
 // Wait for fused batches by polling their completion word (XS_ENGINE_SPIN=0: the event only),
 // for at most kSpinNs before falling back to a blocking event wait.
 constexpr int64_t kSpinNs = 200000;
+// Pure spinning only for about one fused batch's round trip; past it the poll yields the core
+// between checks, so that waiters do not starve the callers' own threads when there are more
+// runnable threads than cores (16 concurrent readers on a 16-core share).
+static int64_t spin_pure_ns() {
+  static const int64_t ns = [] {
+    const char* v = getenv("XS_SPIN_PURE_US");
+    return (v ? atoll(v) : 30) * 1000;
+  }();
+  return ns;
+}
 static bool spin_wait() {
   static const bool on = [] {
     const char* v = getenv("XS_ENGINE_SPIN");
@@ -767,8 +786,6 @@ static int engine_issue_zero_copy(xs_engine::CSlot& c, const std::vector<uint64_
                              spin_wait() ? c.d_ctr : nullptr, (uint32_t*)(uintptr_t)c.d_h_flag, c.seq, st);
     c.spin = spin_wait();
     if (err != hipSuccess) return hip_fail(err, "zero-copy fused");
-    err = hipEventRecord(c.done, st);
-    if (err != hipSuccess) return hip_fail(err, "zero-copy event");
     return XS_OK;
   }
   for (size_t r = 0; r < batch.size();) {  // one keygen per run of (direction, key)
@@ -790,12 +807,12 @@ static int engine_issue_zero_copy(xs_engine::CSlot& c, const std::vector<uint64_
     err = launch_crypt(false, c.keys + nseal, nblk - nseal, src, dst, (uint8_t*)(uintptr_t)c.d_h_ok + nseal, st);
     if (err != hipSuccess) return hip_fail(err, "zero-copy open");
   }
-  err = hipEventRecord(c.done, st);
-  if (err != hipSuccess) return hip_fail(err, "zero-copy event");
   return XS_OK;
 }
 
-// Issue one combined batch on coalescing slot c (asynchronously; completion = c.done).
+// Issue one combined batch on coalescing slot c (asynchronously).  The slot's stream carries only
+// this batch, so the stream's completion is the batch's: no event is recorded (one runtime call
+// less per batch; concurrent callers' launches serialise inside the runtime).
 static int engine_issue_batch(xs_engine* e, xs_engine::CSlot& c) {
   auto& batch = c.batch;
   c.spin = false;  // only a fused zero-copy launch sets it
@@ -877,7 +894,6 @@ static int engine_issue_batch(xs_engine* e, xs_engine::CSlot& c) {
     if (err == hipSuccess && !batch[r]->seal)
       err = hipMemcpyAsync(batch[r]->ok, c.ok + blk0[r], batch[r]->nblocks, hipMemcpyDeviceToHost, st);
   }
-  if (err == hipSuccess) err = hipEventRecord(c.done, st);
   if (err != hipSuccess) return hip_fail(err, "coalesced D2H");
   return XS_OK;
 }
@@ -893,19 +909,23 @@ static void engine_wait_batch(xs_engine::CSlot& c) {
       // bounded: a fused batch takes tens of microseconds; past kSpinNs (a busy GPU) the
       // waiter blocks on the event instead of burning a core
       const auto t0 = std::chrono::steady_clock::now();
+      bool yielding = false;
       for (unsigned k = 1;; k++) {
         if (__atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) == c.seq) {
           seen = true;
           break;
         }
-        __builtin_ia32_pause();
-        if ((k & 255u) == 0) {
-          if (hipEventQuery(c.done) != hipErrorNotReady) break;
-          if (std::chrono::steady_clock::now() - t0 > std::chrono::nanoseconds(kSpinNs)) break;
+        if (yielding) std::this_thread::yield();
+        else __builtin_ia32_pause();
+        if ((k & 255u) == 0 || yielding) {
+          if ((k & 15u) == 0 && hipStreamQuery(c.s) != hipErrorNotReady) break;
+          const auto el = std::chrono::steady_clock::now() - t0;
+          if (el > std::chrono::nanoseconds(kSpinNs)) break;
+          yielding = el > std::chrono::nanoseconds(spin_pure_ns());
         }
       }
     }
-    hipError_t err = seen ? hipSuccess : hipEventSynchronize(c.done);
+    hipError_t err = seen ? hipSuccess : hipStreamSynchronize(c.s);
     if (err != hipSuccess) c.rc = hip_fail(err, "coalesced stream");
   } else {
     (void)hipStreamSynchronize(c.s);
@@ -958,9 +978,10 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
   }
   std::unique_lock<std::mutex> lk(e->qmu);
   e->queue.push_back(&req);
+  e->qcount.store(e->queue.size(), std::memory_order_relaxed);
   while (!req.done) {
     if (e->leader) {
-      e->qcv.wait(lk);
+      (e->wake_all ? e->qcv : req.cv).wait(lk);
       continue;
     }
     // lead: keep up to nslots combined batches in flight until our own request is done and
@@ -968,16 +989,22 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
     e->leader = true;
     const size_t ns = e->ncslots;
     size_t head = 0, inflight = 0;  // ring of slots: [head, head + inflight) are in flight
+    // move the queue's head requests (up to one batch) into the next free slot; qmu held
+    auto take_batch = [&]() -> xs_engine::CSlot& {
+      auto& c = e->cslots[(head + inflight) % ns];
+      c.batch.clear();
+      c.blocks = 0;
+      size_t take = 0;
+      while (take < e->queue.size() && c.blocks + e->queue[take]->nblocks <= e->c_cap_blocks)
+        c.blocks += e->queue[take++]->nblocks;
+      c.batch.assign(e->queue.begin(), e->queue.begin() + take);
+      e->queue.erase(e->queue.begin(), e->queue.begin() + take);
+      e->qcount.store(e->queue.size(), std::memory_order_relaxed);
+      return c;
+    };
     while (!(req.done && inflight == 0)) {
       if (inflight < ns && !e->queue.empty() && !req.done) {
-        auto& c = e->cslots[(head + inflight) % ns];
-        c.batch.clear();
-        c.blocks = 0;
-        size_t take = 0;
-        while (take < e->queue.size() && c.blocks + e->queue[take]->nblocks <= e->c_cap_blocks)
-          c.blocks += e->queue[take++]->nblocks;
-        c.batch.assign(e->queue.begin(), e->queue.begin() + take);
-        e->queue.erase(e->queue.begin(), e->queue.begin() + take);
+        auto& c = take_batch();
         lk.unlock();
         c.rc = engine_issue_batch(e, c);
         lk.lock();
@@ -987,11 +1014,37 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
       if (inflight == 0) break;  // nothing queued for us (own request already done)
       auto& c = e->cslots[head];
       lk.unlock();
+      if (e->overlap) {
+        // wait for the head batch, but put requests that arrive meanwhile into free slots at once
+        // (they would otherwise wait for the head's whole round trip before being issued)
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned k = 1; c.rc == XS_OK; k++) {
+          if (c.spin && __atomic_load_n(c.h_flag, __ATOMIC_ACQUIRE) == c.seq) break;
+          if (inflight < ns && !req.done && e->qcount.load(std::memory_order_relaxed) != 0) {
+            lk.lock();
+            if (!e->queue.empty()) {
+              auto& n = take_batch();
+              lk.unlock();
+              n.rc = engine_issue_batch(e, n);
+              inflight++;
+            } else {
+              lk.unlock();
+            }
+            continue;
+          }
+          __builtin_ia32_pause();
+          if ((k & 255u) == 0) {
+            if (hipStreamQuery(c.s) != hipErrorNotReady) break;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::nanoseconds(kSpinNs)) break;
+          }
+        }
+      }
       engine_wait_batch(c);
       lk.lock();
       for (auto* q : c.batch) {
         q->rc = c.rc;
         q->done = true;
+        if (!e->wake_all) q->cv.notify_one();  // under qmu: the waiter cannot return (and its request vanish) first
       }
       e->st_batches++;
       e->st_reqs += c.batch.size();
@@ -999,10 +1052,11 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
       c.batch.clear();
       head = (head + 1) % ns;
       inflight--;
-      e->qcv.notify_all();
+      if (e->wake_all) e->qcv.notify_all();
     }
     e->leader = false;
-    e->qcv.notify_all();  // a waiting caller with a queued request takes over the lead
+    if (e->wake_all) e->qcv.notify_all();
+    else if (!e->queue.empty()) e->queue.front()->cv.notify_one();  // it takes over the lead
   }
   return req.rc;
 }

@@ -147,7 +147,10 @@ print(json.dumps({"bad": bad[:10], "nbad": len(bad), "cases": cases, "digest": h
 
 
 def _run(version):
-    env = dict(os.environ, XS_FUSED_V=str(version), XS_ENGINE_ZERO_COPY="1", XS_ENGINE_COALESCE="1")
+    # the leader holds new requests while a batch is in flight and express lanes are off, so the
+    # concurrent phase forms multi-request fused batches (the path this test is about)
+    env = dict(os.environ, XS_FUSED_V=str(version), XS_ENGINE_ZERO_COPY="1", XS_ENGINE_COALESCE="1",
+               XS_ENGINE_OVERLAP="0", XS_EXPRESS_MAX="0")
     r = subprocess.run([sys.executable, "-c", SCRIPT % {"root": ROOT}], capture_output=True, text=True, timeout=240,
                        env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]

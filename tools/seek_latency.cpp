@@ -102,11 +102,15 @@ int main(int argc, char** argv) {
   Store st{ct.data(), (int64_t)ct.size()};
   std::vector<std::vector<double>> lat(threads);
   std::atomic<int64_t> bad{0};
+  // per-phase time sums (microseconds): seek-open, read, close + free
+  std::atomic<int64_t> ph_open{0}, ph_read{0}, ph_close{0};
   auto one = [&](uint64_t& rs, std::vector<uint8_t>& buf) {
     const int64_t off = (int64_t)(splitmix(rs) % (uint64_t)(size - len + 1));
     const double t0 = now();
     int32_t e = 0;
     rc_decrypter* d = rc_decrypt_data_seek(c, open_range, &st, off, len, &e);
+    const double t1 = now();
+    double t2 = t1;
     int64_t got = 0;
     if (d) {
       for (;;) {
@@ -114,10 +118,14 @@ int main(int argc, char** argv) {
         got += k;
         if (e != RC_NIL || got == len) break;
       }
+      t2 = now();
       rc_decrypter_close(d);
       rc_decrypter_free(d);
     }
     const double dt = now() - t0;
+    ph_open += (int64_t)((t1 - t0) * 1e6);
+    ph_read += (int64_t)((t2 - t1) * 1e6);
+    ph_close += (int64_t)((t0 + dt - t2) * 1e6);
     if (got != len || memcmp(buf.data(), plain.data() + off, (size_t)len)) {
       if (bad++ < 4) {
         int64_t first = -1;
@@ -150,6 +158,9 @@ int main(int argc, char** argv) {
   auto pct = [&](double p) { return all.empty() ? 0.0 : all[std::min(all.size() - 1, (size_t)(p * all.size()))] * 1e6; };
   const char* sm = getenv("XS_SPLIT_MAX");
   printf("{\"split_max_env\": \"%s\", \"p25_us\": %.1f, \"p75_us\": %.1f, ", sm ? sm : "", pct(0.25), pct(0.75));
+  const double nr = (double)std::max<size_t>(all.size() + 20, 1);
+  printf("\"mean_open_us\": %.1f, \"mean_read_us\": %.1f, \"mean_close_us\": %.1f, ", ph_open / nr, ph_read / nr,
+         ph_close / nr);
   printf("\"tool\": \"seek_latency\", \"object_mib\": %lld, \"read_len\": %lld, \"threads\": %d, \"reads\": %zu, "
          "\"p50_us\": %.1f, \"p90_us\": %.1f, \"p99_us\": %.1f, \"reads_per_s\": %.0f, \"bad\": %lld}\n",
          (long long)mib, (long long)len, threads, all.size(), pct(0.5), pct(0.9), pct(0.99), all.size() / el,
