@@ -42,7 +42,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=60, help="timed steps (about 0.4 s at N=1)")
     ap.add_argument("--warmup", type=int, default=10, help="untimed steps (at least --warmup-seconds of them)")
     ap.add_argument("--warmup-seconds", type=float, default=2.0,
                     help="minimum back-to-back warm-up time: the DVFS clock settles after >= 2 s of load "
