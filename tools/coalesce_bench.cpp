@@ -34,7 +34,7 @@ int main(int argc, char** argv) {
   int32_t e = 0;
   rc_cipher* c = rc_cipher_new("potato", "", &e);
   if (!c) return 1;
-  rc_cipher_set_batch_blocks(c, 64);
+  rc_cipher_set_batch_blocks(c, argc > 5 ? (uint32_t)atoi(argv[5]) : 64);  // argv[5]: batch blocks per refill
   if (argc > 4) rc_cipher_set_readahead(c, (uint32_t)atoi(argv[4]));
   std::vector<uint8_t> src((size_t)S);
   for (int64_t i = 0; i < S; i++) src[(size_t)i] = (uint8_t)(i * 7 + 3);
