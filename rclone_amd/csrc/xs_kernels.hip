@@ -1767,6 +1767,23 @@ xs_open(const BlockKey* __restrict__ keys, uint64_t nblocks, const uint8_t* __re
 // Tiny descriptor batches (ranged reads): keygen and the split crypt kernel in one launch.  Wave 0
 // builds the block's key schedule in LDS (keygen_wave), then the four waves seal / open it as
 // xs_seal_split / xs_open_split do.  Saves the second launch and the key schedule's HBM round trip.
+// Completion word of a fused batch (every wave of every workgroup reaches it): each wave's outputs
+// are fenced at system scope; a one-block batch has no other workgroup to count, otherwise the last
+// workgroup to arrive signals.  The system-scope release of the word orders it after this
+// workgroup's fenced outputs and, through the acq_rel counter, after every other workgroup's.
+__device__ __forceinline__ void xs_fused_complete(uint32_t* ctr, uint32_t* flag, uint32_t seq, uint64_t nblocks) {
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const bool last = nblocks == 1u ||
+                      __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nblocks - 1u;
+    if (last) {
+      if (nblocks != 1u) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 template <bool SEAL>
 __global__ void __launch_bounds__(256) xs_crypt_fused(KeyArg key, NonceArg bounds, const xs_block_desc* __restrict__ desc,
                                                       uint64_t nblocks, const uint8_t* __restrict__ src,
@@ -1780,18 +1797,7 @@ __global__ void __launch_bounds__(256) xs_crypt_fused(KeyArg key, NonceArg bound
   if (threadIdx.x < 64) keygen_wave<SEAL ? 2 : 3>(key, bounds, 0, 0, desc, blockIdx.x, &kl, pw);
   __syncthreads();
   crypt_wave<SEAL, 4, true>(&kl, nblocks, src, dst, ok, lds);
-  if (ctr) {  // completion word: every wave's outputs at system scope, then the last workgroup signals
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == (uint32_t)nblocks - 1u) {
-        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __threadfence_system();
-        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-  }
+  if (ctr) xs_fused_complete(ctr, flag, seq, nblocks);
 }
 
 // Tiny descriptor batches, latency-first (XS_FUSED_V 3, default; 2 = the four-crypt-wave form):
@@ -2201,18 +2207,7 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
       F2_MARK(14);
     }
   }
-  if (ctr) {  // completion word: every wave's outputs at system scope, then the last workgroup signals
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == (uint32_t)nblocks - 1u) {
-        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __threadfence_system();
-        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-  }
+  if (ctr) xs_fused_complete(ctr, flag, seq, nblocks);
 }
 
 __global__ void __launch_bounds__(256) xs_seal_split(const BlockKey* __restrict__ keys, uint64_t nblocks,

@@ -1,6 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-for t in 1 4; do for bb in 64 256; do
-  echo "threads $t batch $bb: $(timeout -k 10 60 ./tools/coalesce_bench $t 32 8388608 0 $bb | cut -c1-200)"
-  echo "threads $t batch $bb 64MiB: $(timeout -k 10 60 ./tools/coalesce_bench $t 8 67108864 0 $bb | cut -c1-200)"
-done; done
+timeout -k 10 900 python -u -m pytest -x -q --timeout 500 --timeout-method thread -p no:cacheprovider tests/test_fused_gpu.py tests/test_engine_coalesce_gpu.py tests/test_cipher_gpu.py tests/test_gpu_parity.py > gpurun_out/r02ba.tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/r02ba.tests.log; exit 1; }
+tail -1 gpurun_out/r02ba.tests.log
