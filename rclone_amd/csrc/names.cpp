@@ -135,19 +135,81 @@ struct Err {
 const char kB32Hex[] = "0123456789ABCDEFGHIJKLMNOPQRSTUV";
 const char kB64Url[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
 
-// base32.HexEncoding.EncodeToString, '=' trimmed, lower-cased (cipher.go:136-140).
+const char kB32HexLower[] = "0123456789abcdefghijklmnopqrstuv";
+
+// base32.HexEncoding.EncodeToString, '=' trimmed, lower-cased (cipher.go:136-140): five bytes
+// to eight characters per step, written in place.
 void enc_base32(const uint8_t* p, size_t n, std::string& o) {
+  const size_t at = o.size();
+  o.resize(at + (n * 8 + 4) / 5);  // unpadded length: 2, 4, 5, 7 characters for a 1..4-byte tail
+  char* d = &o[at];
+  size_t i = 0;
+  for (; i + 5 <= n; i += 5, d += 8) {
+    const uint64_t v = (uint64_t)p[i] << 32 | (uint64_t)p[i + 1] << 24 | (uint64_t)p[i + 2] << 16 |
+                       (uint64_t)p[i + 3] << 8 | p[i + 4];
+    for (int k = 0; k < 8; k++) d[k] = kB32HexLower[(v >> (35 - 5 * k)) & 31];
+  }
   uint64_t acc = 0;
   int bits = 0;
-  for (size_t i = 0; i < n; i++) {
+  for (; i < n; i++) {
     acc = (acc << 8) | p[i];
     bits += 8;
     while (bits >= 5) {
       bits -= 5;
-      o += (char)tolower(kB32Hex[(acc >> bits) & 31]);
+      *d++ = kB32HexLower[(acc >> bits) & 31];
     }
   }
-  if (bits) o += (char)tolower(kB32Hex[(acc << (5 - bits)) & 31]);
+  if (bits) *d++ = kB32HexLower[(acc << (5 - bits)) & 31];
+}
+
+// Value of a base32hex character after strings.ToUpper (either case accepted), or -1.
+const std::array<int8_t, 256>& b32_values() {
+  static const std::array<int8_t, 256> m = [] {
+    std::array<int8_t, 256> t;
+    t.fill(-1);
+    for (int i = 0; i < 32; i++) {
+      t[(uint8_t)kB32Hex[i]] = (int8_t)i;
+      t[(uint8_t)kB32HexLower[i]] = (int8_t)i;
+    }
+    return t;
+  }();
+  return m;
+}
+
+// dec_base32 for the inputs EncodeToString produces: every byte a base32hex character in
+// either case and a length whose unpadded tail is 0, 2, 4, 5 or 7 characters.  Then padding,
+// upper-casing and newline stripping change nothing and encoding/base32 decodes quantum by
+// quantum, ignoring a tail's unused low bits (non-strict).  False: take the exact path.
+bool dec_base32_fast(const char* s, size_t n, std::vector<uint8_t>& out) {
+  const size_t r = n & 7;
+  if (r == 1 || r == 3 || r == 6) return false;
+  const auto& v = b32_values();
+  const uint8_t* p = (const uint8_t*)s;
+  out.resize(n / 8 * 5 + (r * 5) / 8);
+  uint8_t* d = out.data();
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8, d += 5) {
+    uint64_t acc = 0;
+    int bad = 0;
+    for (int k = 0; k < 8; k++) {
+      const int8_t x = v[p[i + k]];
+      bad |= x;
+      acc = acc << 5 | (uint8_t)x;
+    }
+    if (bad < 0) return false;
+    for (int k = 0; k < 5; k++) d[k] = (uint8_t)(acc >> (32 - 8 * k));
+  }
+  if (r) {
+    uint64_t acc = 0;
+    for (size_t k = 0; k < r; k++) {
+      const int8_t x = v[p[i + k]];
+      if (x < 0) return false;
+      acc = acc << 5 | (uint8_t)x;
+    }
+    acc <<= 5 * (8 - r);
+    for (size_t k = 0; k < (r * 5) / 8; k++) d[k] = (uint8_t)(acc >> (32 - 8 * k));
+  }
+  return true;
 }
 
 // caseInsensitiveBase32Encoding.DecodeString (cipher.go:143-152) over encoding/base32's
@@ -156,13 +218,28 @@ void enc_base32(const uint8_t* p, size_t n, std::string& o) {
 Err dec_base32(const char* s0, size_t n0, std::vector<uint8_t>& out) {
   out.clear();
   if (n0 && s0[n0 - 1] == '=') return {RC_ERR_BAD_BASE32_ENCODING, 0};
-  size_t equals = ((n0 + 7) & ~(size_t)7) - n0;
+  if (dec_base32_fast(s0, n0, out)) return {};
+  out.clear();
+  size_t equals = ((n0 + 7) & ~(size_t)7) - n0;  // from the length before ToUpper, as in Go
   thread_local std::string s;
   s.clear();
   s.reserve(n0 + equals);
   for (size_t q = 0; q < n0; q++) {
     char ch = s0[q];
     if (ch == '\r' || ch == '\n') continue;  // stripNewlines
+    // strings.ToUpper maps two non-ASCII runes onto the alphabet: U+0131 'ı' -> 'I' and U+017F
+    // 'ſ' -> 'S' (two bytes become one, so the padding computed above no longer fits).  Every
+    // other non-ASCII rune stays outside the alphabet and fails at the same offset.
+    if (q + 1 < n0 && (uint8_t)ch == 0xC4 && (uint8_t)s0[q + 1] == 0xB1) {
+      s += 'I';
+      q++;
+      continue;
+    }
+    if (q + 1 < n0 && (uint8_t)ch == 0xC5 && (uint8_t)s0[q + 1] == 0xBF) {
+      s += 'S';
+      q++;
+      continue;
+    }
     s += (ch >= 'a' && ch <= 'z') ? (char)(ch - 32) : ch;
   }
   s.append(equals, '=');
@@ -209,9 +286,20 @@ Err dec_base32(const char* s0, size_t n0, std::vector<uint8_t>& out) {
 
 // base64.RawURLEncoding.EncodeToString
 void enc_base64(const uint8_t* p, size_t n, std::string& o) {
+  const size_t at = o.size();
+  o.resize(at + n / 3 * 4);
+  char* d = &o[at];
+  size_t i = 0;
+  for (; i + 3 <= n; i += 3, d += 4) {  // three bytes to four characters per step
+    const uint32_t v = (uint32_t)p[i] << 16 | (uint32_t)p[i + 1] << 8 | p[i + 2];
+    d[0] = kB64Url[v >> 18];
+    d[1] = kB64Url[(v >> 12) & 63];
+    d[2] = kB64Url[(v >> 6) & 63];
+    d[3] = kB64Url[v & 63];
+  }
   uint32_t acc = 0;
   int bits = 0;
-  for (size_t i = 0; i < n; i++) {
+  for (; i < n; i++) {
     acc = (acc << 8) | p[i];
     bits += 8;
     while (bits >= 6) {
@@ -232,6 +320,33 @@ Err dec_base64(const char* s, size_t sn, std::vector<uint8_t>& out) {
     for (int i = 0; i < 64; i++) m[(uint8_t)kB64Url[i]] = (int8_t)i;
     return m;
   }();
+  // Inputs EncodeToString produces (every byte in the alphabet, no 1-character tail) decode
+  // four characters to three bytes per step; anything else takes the exact quantum decoder.
+  if (sn % 4 != 1) {
+    const uint8_t* p = (const uint8_t*)s;
+    const size_t r = sn % 4;
+    out.resize(sn / 4 * 3 + (r ? r - 1 : 0));
+    uint8_t* d = out.data();
+    size_t i = 0;
+    int bad = 0;
+    for (; i + 4 <= sn; i += 4, d += 3) {
+      const int8_t a = map[p[i]], b = map[p[i + 1]], c = map[p[i + 2]], e = map[p[i + 3]];
+      bad |= a | b | c | e;
+      const uint32_t v = (uint32_t)(uint8_t)a << 18 | (uint32_t)(uint8_t)b << 12 | (uint32_t)(uint8_t)c << 6 | (uint8_t)e;
+      d[0] = (uint8_t)(v >> 16);
+      d[1] = (uint8_t)(v >> 8);
+      d[2] = (uint8_t)v;
+    }
+    uint32_t v = 0;
+    for (size_t k = 0; k < r; k++) {
+      const int8_t a = map[p[i + k]];
+      bad |= a;
+      v |= (uint32_t)(uint8_t)a << (18 - 6 * k);
+    }
+    for (size_t k = 0; k + 1 < r; k++) d[k] = (uint8_t)(v >> (16 - 8 * k));
+    if (bad >= 0) return {};
+    out.clear();
+  }
   size_t si = 0;
   while (si < sn) {
     uint8_t d[4] = {0};
@@ -376,8 +491,13 @@ bool version_at(const char* p) {
 }
 
 bool version_match(const char* p, size_t n) {
-  for (size_t st = 0; st + kVersionLen <= n; st++)
-    if (p[st] == '-' && version_at(p + st)) return true;
+  if (n < kVersionLen) return false;
+  const char* const last = p + (n - kVersionLen);  // the latest start a version fits at
+  for (const char* q = p; q <= last; q++) {
+    q = (const char*)memchr(q, '-', (size_t)(last - q) + 1);
+    if (!q) return false;
+    if (version_at(q)) return true;
+  }
   return false;
 }
 
@@ -916,6 +1036,12 @@ int32_t rc_names_run(rc_cipher* c, int32_t op, uint64_t n, const char* const* in
     Chunk& ch = r->chunks[ci];
     uint64_t i0 = ci * kChunkNames, i1 = std::min<uint64_t>(n, i0 + kChunkNames);
     ch.segs.reserve(i1 - i0);
+    ch.seg0.reserve(i1 - i0);
+    ch.direct.reserve(i1 - i0);
+    ch.roff.reserve(i1 - i0);
+    ch.rlen.reserve(i1 - i0);
+    ch.err.reserve(i1 - i0);
+    ch.batch.desc.reserve(i1 - i0);
     ch.batch.data.reserve((i1 - i0) * 48);
     for (uint64_t i = i0; i < i1; i++) prepare_input(x, ch, in[i], in_len[i]);
   });
