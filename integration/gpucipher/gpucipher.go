@@ -108,6 +108,7 @@ func (t *errTable) err(code C.int32_t) error {
 type readerBox struct {
 	r io.Reader
 	t *errTable
+	s *openState // the decrypter's state (its RangeSeek context), nil for an encrypter's source
 }
 
 //export goRead
@@ -132,7 +133,15 @@ func goClose(h C.uintptr_t) C.int32_t {
 func goRangeSeek(h C.uintptr_t, offset C.int64_t, whence C.int32_t, limit C.int64_t) C.int32_t {
 	b := cgo.Handle(h).Value().(*readerBox)
 	rs := b.r.(fs.RangeSeeker) // only registered when the reader is one (cipher.go:997)
-	_, err := rs.RangeSeek(context.TODO(), int64(offset), int(whence), int64(limit))
+	ctx := context.TODO()
+	if b.s != nil {
+		b.s.mu.Lock()
+		if b.s.ctx != nil {
+			ctx = b.s.ctx // the ctx of the Decrypter.RangeSeek call in progress (cipher.go:999)
+		}
+		b.s.mu.Unlock()
+	}
+	_, err := rs.RangeSeek(ctx, int64(offset), int(whence), int64(limit))
 	return b.t.code(err)
 }
 
@@ -148,7 +157,7 @@ type openState struct {
 }
 
 func (s *openState) newReader(r io.Reader, closer bool) C.rc_reader {
-	hd := cgo.NewHandle(&readerBox{r: r, t: s.t})
+	hd := cgo.NewHandle(&readerBox{r: r, t: s.t, s: s})
 	s.mu.Lock()
 	s.handles = append(s.handles, hd)
 	s.mu.Unlock()
