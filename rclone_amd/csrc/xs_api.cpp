@@ -355,6 +355,7 @@ struct xs_engine {
   bool overlap = false;           // XS_ENGINE_OVERLAP=1: the leader issues newly queued requests while it
                                   // waits (lower latency at low load, less coalescing: off by default)
   bool wake_all = false;          // XS_ENGINE_WAKE_ALL=1: one shared condition, every waiter woken (A/B)
+  bool one_run = true;            // a combined batch holds one (direction, key) run (XS_BATCH_ONE_RUN=0: mixed)
   std::condition_variable qcv;    // the shared condition of wake_all
   bool leader = false;
   struct CSlot {  // one combined batch in flight
@@ -557,6 +558,7 @@ extern "C" xs_engine* xs_engine_create(int device, uint32_t batch_blocks, int ns
   if (const char* v = getenv("XS_EXPRESS_MAX")) e->express_max = strtoull(v, nullptr, 10);
   if (const char* v = getenv("XS_ENGINE_OVERLAP")) e->overlap = atoi(v) != 0;
   if (const char* v = getenv("XS_ENGINE_WAKE_ALL")) e->wake_all = atoi(v) != 0;
+  if (const char* v = getenv("XS_BATCH_ONE_RUN")) e->one_run = atoi(v) != 0;
   return e;
 }
 
@@ -994,11 +996,28 @@ static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const u
       auto& c = e->cslots[(head + inflight) % ns];
       c.batch.clear();
       c.blocks = 0;
-      size_t take = 0;
-      while (take < e->queue.size() && c.blocks + e->queue[take]->nblocks <= e->c_cap_blocks)
-        c.blocks += e->queue[take++]->nblocks;
-      c.batch.assign(e->queue.begin(), e->queue.begin() + take);
-      e->queue.erase(e->queue.begin(), e->queue.begin() + take);
+      if (e->one_run) {
+        // one (direction, key) run per batch: a small batch then stays one fused launch instead
+        // of keygen + crypt per direction; requests of the other run keep their queue order
+        const xs_engine::Req* f = e->queue.front();
+        size_t keep = 0;
+        for (size_t i = 0; i < e->queue.size(); i++) {
+          auto* q = e->queue[i];
+          if (q->seal == f->seal && !memcmp(q->key, f->key, 32) && c.blocks + q->nblocks <= e->c_cap_blocks) {
+            c.blocks += q->nblocks;
+            c.batch.push_back(q);
+          } else {
+            e->queue[keep++] = q;
+          }
+        }
+        e->queue.resize(keep);
+      } else {
+        size_t take = 0;
+        while (take < e->queue.size() && c.blocks + e->queue[take]->nblocks <= e->c_cap_blocks)
+          c.blocks += e->queue[take++]->nblocks;
+        c.batch.assign(e->queue.begin(), e->queue.begin() + take);
+        e->queue.erase(e->queue.begin(), e->queue.begin() + take);
+      }
       e->qcount.store(e->queue.size(), std::memory_order_relaxed);
       return c;
     };
