@@ -78,7 +78,9 @@ xs_pool* process_pool() {
   if (g_xs_pool || g_xs_pool_failed) return g_xs_pool;
   uint32_t batch = 256;
   if (const char* s = getenv("RCLONE_AMD_ENGINE_BLOCKS")) batch = (uint32_t)atoi(s);
-  g_xs_pool = xs_pool_create(nullptr, 0, batch, 3);
+  int slots = 3;  // combined batches in flight per engine
+  if (const char* s = getenv("RCLONE_AMD_ENGINE_SLOTS")) slots = std::max(1, std::min(16, atoi(s)));
+  g_xs_pool = xs_pool_create(nullptr, 0, batch, slots);
   if (!g_xs_pool) g_xs_pool_failed = true;
   return g_xs_pool;
 }
