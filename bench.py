@@ -228,7 +228,7 @@ def run_objectset(args, world, rank, dev, dist):
                        "parallelism": f"{world} rank(s), blocks sharded, counters all-reduced"},
             "seal_kernel_GiB_s": round(r.n * BLOCK_DATA * args.steps / 2**30 / (sum(seal_ms) * 1e-3), 3),
             "open_kernel_GiB_s": round(r.n * BLOCK_DATA * args.steps / 2**30 / (sum(open_ms) * 1e-3), 3),
-            "counters": {"blocks": blocks, "bytes": nbytes, "tag_failures": fails, "roundtrip_mismatch_rounds": mism,
+            "counters": {"blocks": blocks, "bytes": nbytes, "tag_failures": fails, "roundtrip_mismatch_words": mism,
                          "tag_digest": f"{d1:016x}{d0:016x}"},
             "roofline": None, "cpu_baseline": None,
         }

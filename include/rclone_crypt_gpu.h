@@ -123,6 +123,11 @@ int xs_fill_random_dev(void *d, uint64_t nbytes, uint64_t seed, void *stream);
  * same stream (a rank's round-robin share of a synthetic object set, BASELINE configs[3]). */
 int xs_fill_blocks_dev(void *d, uint64_t nblocks, uint64_t first_block, uint64_t block_stride, uint64_t seed,
                        void *stream);
+/* Check nblocks 64 KiB blocks at d against the stream xs_fill_blocks_dev(.., first_block,
+ * block_stride, seed) writes: the number of differing 64-bit words is added to *d_mismatch (device
+ * memory, 8-byte aligned).  The object-set benchmark's round-trip check. */
+int xs_verify_blocks_dev(const void *d, uint64_t nblocks, uint64_t first_block, uint64_t block_stride, uint64_t seed,
+                         uint64_t *d_mismatch, void *stream);
 
 /* Shader-clock probe (benchmarking): one wave on `stream` records s_memtime against the 100 MHz
  * s_memrealtime until *d_stop (device memory, 0 at launch) becomes non-zero or max_seconds pass;

@@ -56,6 +56,7 @@ _SIGS = [
     ("xs_keygen_batch_dev", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, vp, u64, vp, u64, vp, u64, vp, vp]),
     ("xs_fill_random_dev", ctypes.c_int, [vp, u64, u64, vp]),
     ("xs_fill_blocks_dev", ctypes.c_int, [vp, u64, u64, u64, u64, vp]),
+    ("xs_verify_blocks_dev", ctypes.c_int, [vp, u64, u64, u64, u64, vp, vp]),
     ("xs_md5_batch_dev", ctypes.c_int, [vp, u64, vp, u64, vp, vp, vp]),
     ("xs_clock_probe_dev", ctypes.c_int, [vp, vp, ctypes.c_double, vp]),
     ("xs_engine_create", vp, [ctypes.c_int, ctypes.c_uint32, ctypes.c_int]),

@@ -1,4 +1,5 @@
-// xs_probe.hip -- in-window shader clock probe for the benchmark (bench.py).
+// xs_probe.hip -- benchmark utilities: the in-window shader clock probe (bench.py) and the
+// round-trip check of synthetic SplitMix64 objects (the object-set mode, BASELINE configs[3]).
 //
 // One wave runs beside the crypt kernels on its own stream and records the shader clock counter
 // (s_memtime) against the 100 MHz constant clock (s_memrealtime) at its start and then every
@@ -33,7 +34,47 @@ __global__ void __launch_bounds__(64) xs_clock_probe(const volatile uint32_t* st
   }
 }
 
+// Round-trip check of a synthetic object set: counts the 64-bit words of src that differ from
+// the SplitMix64 stream xs_fill_splitmix (xs_kernels.hip) wrote -- the same formula and block
+// layout (local 64 KiB block b = global block first_block + b*stride) -- into *mismatch.  Reading
+// the opened plaintext alone halves the check's HBM bytes against comparing it with a kept copy.
+// A lane adds its count with a vector atomic only when it found a mismatch.
+__global__ void __launch_bounds__(256) xs_verify_splitmix(const uint64_t* __restrict__ src, uint64_t nwords,
+                                                          uint64_t seed, uint64_t first_block, uint64_t stride,
+                                                          unsigned long long* __restrict__ mismatch) {
+  uint32_t bad = 0;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nwords;
+       k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t g = (first_block + (k >> 13) * stride) * 8192u + (k & 8191u);
+    uint64_t z = seed + (g + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    bad += src[k] != (z ^ (z >> 31)) ? 1u : 0u;
+  }
+  if (bad) atomicAdd(mismatch, (unsigned long long)bad);
+}
+
 }  // namespace
+
+extern "C" int xs_verify_blocks_dev(const void* d, uint64_t nblocks, uint64_t first_block, uint64_t block_stride,
+                                    uint64_t seed, uint64_t* d_mismatch, void* stream) {
+  if (!d || ((uintptr_t)d & 7u) || !d_mismatch || ((uintptr_t)d_mismatch & 7u) || block_stride == 0) {
+    xs::set_error("xs_verify_blocks_dev: need 8-byte aligned buffers and block_stride >= 1");
+    return XS_ERR_INVALID;
+  }
+  const uint64_t nwords = nblocks * 8192u;
+  if (nwords == 0) return XS_OK;
+  uint64_t grid = (nwords + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(xs_verify_splitmix, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
+                     (const uint64_t*)d, nwords, seed, first_block, block_stride, (unsigned long long*)d_mismatch);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    xs::set_error("verify launch: %s", hipGetErrorString(e));
+    return XS_ERR_HIP;
+  }
+  return XS_OK;
+}
 
 extern "C" int xs_clock_probe_dev(const uint32_t* d_stop, uint64_t* d_out, double max_seconds, void* stream) {
   if (!d_stop || !d_out || max_seconds <= 0) {

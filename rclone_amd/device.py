@@ -109,6 +109,20 @@ def fill_blocks(t: torch.Tensor, first_block: int, block_stride: int, seed: int)
     return t
 
 
+def verify_blocks(t: torch.Tensor, first_block: int, block_stride: int, seed: int, mismatch: torch.Tensor):
+    """Add to mismatch (one int64 on t's device) the number of 64-bit words of t (whole 64 KiB
+    blocks) that differ from what fill_blocks(t, first_block, block_stride, seed) writes."""
+    _require_gpu(t)
+    nbytes = t.numel() * t.element_size()
+    if nbytes % BLOCK_DATA:
+        raise ValueError("verify_blocks needs whole 64 KiB blocks")
+    if mismatch.dtype != torch.int64 or mismatch.numel() != 1 or mismatch.device != t.device:
+        raise ValueError("verify_blocks: mismatch must be one int64 on the data's device")
+    rc = _lib.lib().xs_verify_blocks_dev(t.data_ptr(), nbytes // BLOCK_DATA, first_block, block_stride, seed,
+                                         ctypes_void(mismatch.data_ptr()), _stream(t))
+    _lib.check(rc, "xs_verify_blocks_dev")
+
+
 def _desc_tensor(desc, device):
     """xs_block_desc array (numpy structured, 48 B/entry, or a uint8 device tensor) on device."""
     if isinstance(desc, torch.Tensor):

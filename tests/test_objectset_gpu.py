@@ -47,3 +47,25 @@ def test_objectset_digest_independent_of_world():
         assert (blocks, nbytes, fails, mism) == (TOTAL, TOTAL * 65536, 0, 0), world
         res[world] = (d0, d1)
     assert res[1] == res[2] == res[8]
+
+
+def test_verify_blocks_counts_mismatched_words():
+    # the object set's round-trip check (xs_verify_blocks_dev) recomputes the generator's stream:
+    # zero on the generated blocks (any first_block / stride), and exactly the flipped words
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from rclone_amd import device
+    nb, first, stride = 37, 5, 3
+    t = torch.empty(nb * 65536, dtype=torch.uint8, device="cuda")
+    device.fill_blocks(t, first, stride, SEED)
+    assert t[65536 * 2:65536 * 3].cpu().numpy().tobytes() == splitmix64_block(SEED, first + 2 * stride)
+    m = torch.zeros(1, dtype=torch.int64, device="cuda")
+    device.verify_blocks(t, first, stride, SEED, m)
+    assert int(m) == 0
+    device.verify_blocks(t, first, stride + 1, SEED, m)  # another layout: almost every word differs
+    assert int(m) >= (nb - 1) * 8192
+    m.zero_()
+    for off in (0, 8 * 8191, 65536 * 17 + 8 * 100, nb * 65536 - 8):
+        t[off + 3] ^= 0x40  # one byte in each of four words (block 0 start / end, middle, last word)
+    device.verify_blocks(t, first, stride, SEED, m)
+    assert int(m) == 4
