@@ -166,8 +166,10 @@ def test_concurrent_requests_share_batches(eng, pinned):
                 jobs.append((nonce0, want, bufs))
             ptr = (lambda b: b.p) if pinned else (lambda b: b)
             start.wait()
+            # back to back (the comparisons after): calls overlap instead of queueing on the GIL
+            rcs = [L.xs_engine_seal(e, key, nonce0, 0, ptr(src), n, ptr(body)) for nonce0, _, (src, body) in jobs]
+            assert rcs == [0] * calls
             for nonce0, want, (src, body) in jobs:
-                assert L.xs_engine_seal(e, key, nonce0, 0, ptr(src), n, ptr(body)) == 0
                 assert body.raw == want
         except BaseException as ex:  # noqa: BLE001
             errors.append((t, repr(ex)))
