@@ -24,6 +24,8 @@
 #include <array>
 #include <atomic>
 #include <cctype>
+#include <chrono>
+#include <cstdio>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -1028,6 +1030,15 @@ int32_t rc_names_run(rc_cipher* c, int32_t op, uint64_t n, const char* const* in
               op == RC_OP_OBFUSCATE_SEGMENT;
   x.standard = op == RC_OP_ENCRYPT_SEGMENT || op == RC_OP_DECRYPT_SEGMENT ||
                (op <= RC_OP_DECRYPT_DIR_NAME && c->mode == RC_NAME_STANDARD);
+  // RCLONE_AMD_NAME_TIMING=1: per-phase wall times of each call on stderr (measurement aid)
+  static const bool timing = [] {
+    const char* v = getenv("RCLONE_AMD_NAME_TIMING");
+    return v && atoi(v) != 0;
+  }();
+  const auto t_start = std::chrono::steady_clock::now();
+  auto ms_since = [](std::chrono::steady_clock::time_point a) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+  };
   rc_names* r = new rc_names();
   const size_t nchunks = (n + kChunkNames - 1) / kChunkNames;
   r->chunks.resize(nchunks);
@@ -1045,9 +1056,12 @@ int32_t rc_names_run(rc_cipher* c, int32_t op, uint64_t n, const char* const* in
     ch.batch.data.reserve((i1 - i0) * 48);
     for (uint64_t i = i0; i < i1; i++) prepare_input(x, ch, in[i], in_len[i]);
   });
+  const double t_prep = ms_since(t_start);
   std::vector<SegBatch*> parts(nchunks);
   for (size_t ci = 0; ci < nchunks; ci++) parts[ci] = &r->chunks[ci].batch;
+  const auto t_eme0 = std::chrono::steady_clock::now();
   int32_t rc = run_eme(c, x.enc_dir, parts, &r->kernel_ms);
+  const double t_eme = ms_since(t_eme0);
   if (rc != RC_NIL) {
     delete r;
     return rc;
@@ -1064,6 +1078,10 @@ int32_t rc_names_run(rc_cipher* c, int32_t op, uint64_t n, const char* const* in
     std::string().swap(ch.segout);
     ch.batch = SegBatch();
   });
+  if (timing)
+    fprintf(stderr, "rc_names_run op %d n %llu: prepare %.2f ms, eme (pack + copies + kernel %.2f + unpack) %.2f ms, "
+            "finish %.2f ms\n", (int)op, (unsigned long long)n, t_prep, r->kernel_ms, t_eme,
+            ms_since(t_start) - t_prep - t_eme);
   *out = r;
   return RC_NIL;
 }
