@@ -36,7 +36,7 @@ def test_bench_mixed_objects_mode():
 def test_bench_object_set_mode():
     res = _bench("--object-blocks", "20000", "--blocks", "8192", "--no-cpu")
     assert res["counters"]["blocks"] == 20000 and res["counters"]["tag_failures"] == 0
-    assert res["counters"]["roundtrip_mismatch_rounds"] == 0
+    assert res["counters"]["roundtrip_mismatch_words"] == 0
 
 
 def test_bench_names_mode():
