@@ -97,3 +97,19 @@ def test_splitmix_block_stream():
     whole = splitmix64_bytes(7, 5 * 65536)
     for g in range(5):
         assert splitmix64_block(7, g) == whole[g * 65536:(g + 1) * 65536]
+
+
+def test_device_entry_points_reject_bad_arguments():
+    # argument checks run before any HIP call, so they hold on a machine without a GPU
+    import ctypes
+    lib = _lib.lib()
+    XS_ERR_INVALID = -1  # include/rclone_crypt_gpu.h
+    word = ctypes.c_uint64(0)
+    buf = ctypes.create_string_buffer(65536 + 16)
+    aligned = (ctypes.addressof(buf) + 15) & ~15
+    assert lib.xs_verify_blocks_dev(None, 1, 0, 1, 7, ctypes.byref(word), None) == XS_ERR_INVALID
+    assert "xs_verify_blocks_dev" in _lib.last_error()
+    assert lib.xs_verify_blocks_dev(aligned, 1, 0, 1, 7, None, None) == XS_ERR_INVALID
+    assert lib.xs_verify_blocks_dev(aligned + 4, 1, 0, 1, 7, ctypes.byref(word), None) == XS_ERR_INVALID
+    assert lib.xs_verify_blocks_dev(aligned, 1, 0, 0, 7, ctypes.byref(word), None) == XS_ERR_INVALID
+    assert lib.xs_fill_blocks_dev(aligned, 1, 0, 0, 7, None) == XS_ERR_INVALID
