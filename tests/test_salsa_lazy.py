@@ -69,3 +69,21 @@ def test_generator_is_reproducible():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_salsa_lazy.py")],
                          capture_output=True, text=True, check=True, timeout=600).stdout
     assert out == open(HDR).read()
+
+
+def test_rolled_schedule_is_at_the_dp_bound():
+    # tools/salsa_lazy_bound.py: over every lazy set and the wider move set, the least cost of k
+    # double rounds from cold grows by exactly 82 per double round -- the rolled loop's cost
+    import importlib.util
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    spec = importlib.util.spec_from_file_location("salsa_lazy_bound", os.path.join(ROOT, "tools", "salsa_lazy_bound.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    cur, mins = {0: 0}, []
+    for _ in range(3):
+        cur = mod.layer(cur)
+        mins.append(min(cur.values()))
+    assert mins[0] == 80 and mins[1] - mins[0] == 82 and mins[2] - mins[1] == 82
+    hdr = open(HDR).read()
+    assert "82 VALU ops instead of 96" in hdr
