@@ -19,7 +19,7 @@ SOURCES = ["xs_kernels.hip", "xs_md5.hip", "xs_eme.hip", "xs_probe.hip", "xs_api
 
 # what the crypt kernels (xs_seal / xs_open / keygen) are compiled from: PMC counters committed under
 # profiles/ (tools/make_traffic.py) are valid only for this exact set of bytes
-KERNEL_SOURCES = ["rclone_amd/csrc/xs_kernels.hip", "rclone_amd/csrc/xs_salsa_lazy.h", "rclone_amd/csrc/xs_salsa_asm.h",
+KERNEL_SOURCES = ["rclone_amd/csrc/xs_kernels.hip", "rclone_amd/csrc/xs_salsa_lazy.h",
                   "rclone_amd/csrc/xs_internal.h"]
 
 

@@ -39,9 +39,6 @@
 #ifndef XS_SALSA_LAZY  // Salsa20 double rounds with deferred XORs (v_xad_u32 / v_bitop3_b32)
 #define XS_SALSA_LAZY 1
 #endif
-#ifndef XS_ABL_NOMFMA  // diagnostic ablation only (wrong tags): skip the matrix-core Poly1305 MFMAs
-#define XS_ABL_NOMFMA 0
-#endif
 #ifndef XS_ST_PERM  // output transpose with v_permlane{32,16}_swap instead of the LDS round trip
 #define XS_ST_PERM 0
 #endif
@@ -59,12 +56,6 @@
 #endif
 #ifndef XS_SPLIT_MAX  // batches up to this many blocks run four waves per block (latency)
 #define XS_SPLIT_MAX 256
-#endif
-#ifndef XS_ABL_NOSALSA  // diagnostic ablation only (wrong output): no Salsa20 keystream in the block loop
-#define XS_ABL_NOSALSA 0
-#endif
-#ifndef XS_ABL_NOMEM  // diagnostic ablation only (wrong output): full blocks skip their HBM loads/stores
-#define XS_ABL_NOMEM 0
 #endif
 #ifndef XS_XCD_REMAP
 #define XS_XCD_REMAP 0
@@ -1449,7 +1440,7 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
   // double-buffered staging: group u+1 is requested before group u's keystream is computed
 #pragma unroll
   for (int j = 0; j < 4; j++)
-    if ((j > 0 || not_key) && !XS_ABL_NOMEM)
+    if (j > 0 || not_key)
       __builtin_amdgcn_global_load_lds(pin_m32 + lane_off + 1024 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
 #endif
 #pragma unroll 1
@@ -1462,23 +1453,17 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
       uint32_t* nb = wb + 1024 * ((u + 1) & 1);
 #pragma unroll
       for (int j = 0; j < 4; j++)
-        if (!XS_ABL_NOMEM)
-          __builtin_amdgcn_global_load_lds(pin_m32 + goff + 4096u + 1024 * j, (lds_void*)(nb + 256 * j), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(pin_m32 + goff + 4096u + 1024 * j, (lds_void*)(nb + 256 * j), 16, 0, 0);
     }
 #else
     uint32_t* sb = wb;
 #pragma unroll
     for (int j = 0; j < 4; j++)
-      if ((j > 0 || u > 0 || not_key) && !XS_ABL_NOMEM)
+      if (j > 0 || u > 0 || not_key)
         __builtin_amdgcn_global_load_lds(pin_m32 + goff + 1024 * j, (lds_void*)(sb + 256 * j), 16, 0, 0);
 #endif
     uint32_t ks[16];
-#if XS_ABL_NOSALSA
-#pragma unroll
-    for (int i = 0; i < 16; i++) ks[i] = K * (i + 1);
-#else
     salsa20_block_pre(pre, K, ks);
-#endif
 #if XS_DBUF
     if (u < 15) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // group u landed; u+1 may be in flight
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1512,7 +1497,7 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
       }
 #pragma unroll
       for (int j = 0; j < 4; j++)
-        if ((j > 0 || u > 0 || not_key) && (!XS_ABL_NOMEM || w[4 * j] == 0x12345678u))
+        if (j > 0 || u > 0 || not_key)
           *reinterpret_cast<uint4*>(pout_m32 + goff + 1024 * j) = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
     }
 #else
@@ -1525,8 +1510,7 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
       for (int j = 0; j < 4; j++) w[j] = *reinterpret_cast<const uint4*>(sb + 256 * j + 4 * l);
 #pragma unroll
       for (int j = 0; j < 4; j++)
-        if ((j > 0 || u > 0 || not_key) && (!XS_ABL_NOMEM || w[j].x == 0x12345678u))
-          *reinterpret_cast<uint4*>(pout_m32 + goff + 1024 * j) = w[j];
+        if (j > 0 || u > 0 || not_key) *reinterpret_cast<uint4*>(pout_m32 + goff + 1024 * j) = w[j];
     }
 #endif
     // A operands of row 4u + kg for both output halves
@@ -1548,11 +1532,7 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
       for (int i = 0; i < 4; i++) B[i] = (int)(cw[4 * j + i] ^ 0x80808080u);
 #pragma unroll
       for (int mt = 0; mt < 2; mt++) {
-#if XS_ABL_NOMFMA
-        acc[j][mt] += A[mt] ^ B;
-#else
         acc[j][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[mt], B, acc[j][mt], 0, 0, 0);
-#endif
       }
     }
   }

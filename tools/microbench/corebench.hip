@@ -4,7 +4,7 @@
 #include <cstdio>
 #include <cstdint>
 #include <vector>
-#include "../../rclone_amd/csrc/xs_salsa_asm.h"
+#include "xs_salsa_asm.h"
 
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
 #define QR(a, b, c, d) b ^= rotl(a + d, 7); c ^= rotl(b + a, 9); d ^= rotl(c + b, 13); a ^= rotl(d + c, 18);
