@@ -294,6 +294,13 @@ void rc_nonce_add(uint8_t nonce[24], uint64_t x);      /* :665 */
 rc_encrypter *rc_encrypt_data(rc_cipher *c, rc_reader in, const uint8_t *nonce, int32_t *err);
 int64_t rc_encrypter_read(rc_encrypter *e, uint8_t *p, int64_t n, int32_t *err); /* :719 */
 void rc_encrypter_nonce(const rc_encrypter *e, uint8_t out[24]);
+/* crypt.put's ciphertext hash (crypt.go:516-533: io.TeeReader(wrappedIn, MD5 hasher)) taken by the
+ * encrypter itself, so the Go side drops the TeeReader: call rc_encrypter_set_md5(e, 1) before the
+ * first read (RC_ERR_INVALID after it).  A host worker hashes each sealed batch while the consumer
+ * reads it.  rc_encrypter_md5 returns the MD5 of exactly the bytes returned by rc_encrypter_read so
+ * far -- what hasher.Sums() gives after the wrapped Put -- or RC_ERR_INVALID if the option is off. */
+int32_t rc_encrypter_set_md5(rc_encrypter *e, int32_t on);
+int32_t rc_encrypter_md5(rc_encrypter *e, uint8_t out[16]);
 void rc_encrypter_free(rc_encrypter *e);
 
 /* newDecrypter / DecryptData (:793, :1099) */
@@ -319,6 +326,16 @@ void rc_decrypter_free(rc_decrypter *d);
  * RC_ERR_GPU if the engine failed (no digest valid). */
 int32_t rc_hash_batch_with_nonce(rc_cipher *c, uint64_t n, const rc_reader *srcs, const uint8_t *nonces,
                                  uint8_t *md5, int32_t *errs);
+/* Fs.computeHashWithNonce (crypt.go:784-806) for MD5, one object: the call crypt.go's own
+ * computeHashWithNonce makes, per object, from unchanged cryptcheck / bisync checkers
+ * (cmd/cryptcheck/cryptcheck.go:91-114; concurrency = --checkers).  Reads src to EOF (ReadFill of
+ * one block at a time, as newEncrypter would), seals it on the GPU (concurrent callers' seals are
+ * group-committed into shared launches), MD5s "RCLONE\0\0" || nonce || wire blocks on host cores
+ * (one core hashes a stream ~10x faster than one GPU lane), overlapping batch k's hash with batch
+ * k+1's read and seal, then closes src if it has a close function (defer fs.CheckClose(in, &err)).
+ * Returns RC_NIL with md5 set, the reader's non-EOF error or the closer's error (the reference wraps
+ * them as "failed to hash data: %w"), or RC_ERR_GPU. */
+int32_t rc_compute_hash_with_nonce(rc_cipher *c, rc_reader src, const uint8_t nonce[24], uint8_t md5[16]);
 
 /* ------------------------------------------------------------------------------------
  * File-name cipher (cipher.go:120-618): NameEncryptionMode, fileNameEncoding, encryptSegment /

@@ -101,6 +101,8 @@ _SIGS = [
     ("rc_encrypter_read", i64, [vp, vp, i64, ctypes.POINTER(i32)]),
     ("rc_encrypter_nonce", None, [vp, vp]),
     ("rc_encrypter_free", None, [vp]),
+    ("rc_encrypter_set_md5", i32, [vp, i32]),
+    ("rc_encrypter_md5", i32, [vp, vp]),
     ("rc_decrypt_data", vp, [vp, RcReader, ctypes.POINTER(i32)]),
     ("rc_decrypt_data_seek", vp, [vp, OPEN_FN, vp, i64, i64, ctypes.POINTER(i32)]),
     ("rc_decrypter_read", i64, [vp, vp, i64, ctypes.POINTER(i32)]),
@@ -110,6 +112,7 @@ _SIGS = [
     ("rc_decrypter_wrapped_error", i32, [vp]),
     ("rc_decrypter_free", None, [vp]),
     ("rc_hash_batch_with_nonce", i32, [vp, u64, vp, vp, vp, vp]),
+    ("rc_compute_hash_with_nonce", i32, [vp, RcReader, vp, vp]),
     ("rc_error_string", ctypes.c_char_p, [i32]),
     # file names (cipher.go:120-618)
     ("xs_eme_batch_dev", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, vp, u64, vp, vp, u64, vp]),

@@ -362,11 +362,16 @@ class Cipher(NameCipherMixin):
         return out
 
     def compute_hash_with_nonce(self, nonce: bytes, src) -> str:
-        """computeHashWithNonce (crypt.go:784): MD5 hex of src encrypted with nonce."""
-        r = self.hash_batch_with_nonce([(nonce, src)])[0]
-        if isinstance(r, BaseException):
-            raise r
-        return r.hex()
+        """computeHashWithNonce (crypt.go:784): MD5 hex of src encrypted with nonce, one object per
+        call (rc_compute_hash_with_nonce: GPU seal, group-committed with concurrent callers; MD5
+        on host cores).  src is closed if it has close() (fs.CheckClose); its error is raised."""
+        nb = bytes(nonce)
+        if len(nb) != 24:
+            raise ValueError("nonce must be 24 bytes")
+        bridge = _ReaderBridge(src, closer=True)
+        md5 = ctypes.create_string_buffer(16)
+        _raise(_lib.lib().rc_compute_hash_with_nonce(self._h, bridge.c, nb, md5))
+        return md5.raw.hex()
 
     def compute_hash(self, obj, src) -> str:
         """ComputeHash (crypt.go:816): the nonce comes from the encrypted object's header (read
@@ -438,6 +443,17 @@ class Encrypter:
         b = (ctypes.c_uint8 * 24)()
         _lib.lib().rc_encrypter_nonce(self._h, b)
         return bytes(b)
+
+    def set_md5(self, on: bool = True):
+        """crypt.put's ciphertext tee hash taken by the encrypter (rc_encrypter_set_md5); before
+        the first read only."""
+        _raise(_lib.lib().rc_encrypter_set_md5(self._h, int(bool(on))))
+
+    def md5(self) -> bytes:
+        """MD5 of exactly the bytes read so far (hasher.Sums() of the reference's TeeReader)."""
+        d = ctypes.create_string_buffer(16)
+        _raise(_lib.lib().rc_encrypter_md5(self._h, d))
+        return d.raw
 
     def read_go(self, n):
         """Go-style Read: returns (data, err) with err None, EOF or an exception."""

@@ -131,8 +131,11 @@ class CryptFs:
     """crypt.Fs data path over a wrapped remote (MemoryRemote or anything with the same
     put/open/hash/size/remove)."""
 
-    def __init__(self, wrapped, cipher: crypt.Cipher, ignore_checksum: bool = False):
+    def __init__(self, wrapped, cipher: crypt.Cipher, ignore_checksum: bool = False, encrypter_md5: bool = True):
+        """encrypter_md5: put's tee hash is taken by the encrypter (rc_encrypter_set_md5, hashed on
+        host workers while the wrapped put reads) instead of a TeeReader around it."""
         self.wrapped, self.cipher, self.ignore_checksum = wrapped, cipher, ignore_checksum
+        self.encrypter_md5 = encrypter_md5
 
     @staticmethod
     def enc_name(remote: str) -> str:
@@ -141,14 +144,16 @@ class CryptFs:
     # -------------------------------------------------------------- Fs.put (crypt.go:497)
     def put(self, remote: str, reader, size: int = -1):
         enc = self.cipher.encrypt_data(reader)
-        hasher = None if self.ignore_checksum else hashlib.md5()
+        hasher = None if self.ignore_checksum or self.encrypter_md5 else hashlib.md5()
         src = enc if hasher is None else _TeeReader(enc, hasher)
+        if not self.ignore_checksum and self.encrypter_md5:
+            enc.set_md5(True)
         esize = crypt.encrypted_size(size) if size >= 0 else size  # ObjectInfo.Size (:1168)
         name = self.enc_name(remote)
         nonce = enc.nonce  # newObjectInfo(src, encrypter.nonce) is built before the transfer (:536)
         self.wrapped.put(name, src, esize)
-        if hasher is not None:
-            src_hash = hasher.hexdigest()
+        if not self.ignore_checksum:
+            src_hash = hasher.hexdigest() if hasher is not None else enc.md5().hex()
             dst_hash = self.wrapped.hash(name)
             if src_hash and dst_hash and src_hash != dst_hash:
                 self.wrapped.remove(name)
@@ -198,11 +203,54 @@ class CryptFs:
         return self.cipher.compute_hash_with_nonce(self._nonce(remote), src)
 
     # -------------------------------------------------------------- cryptcheck (cryptcheck.go:67)
-    def cryptcheck(self, sources: dict, batch: int = 4096):
+    def cryptcheck(self, sources: dict, batch: int = 4096, checkers: int = 0):
         """sources: remote -> zero-arg callable returning a reader of the plaintext source.
+        checkers > 0: the unchanged cryptcheck's shape -- that many threads, each running the
+        per-object ComputeHash (cryptcheck.go:91-114, --checkers); else batches of `batch` objects
+        through hash_batch_with_nonce.
         Returns {"differ": [...], "no_hash": [...], "errors": {remote: exc}, "ok": n}."""
         res = {"differ": [], "no_hash": [], "errors": {}, "ok": 0}
         names = sorted(sources)
+        if checkers > 0:
+            import threading
+            lock, it = threading.Lock(), iter(names)
+
+            def check_one(r):
+                try:
+                    under = self.wrapped.hash(self.enc_name(r))
+                except Exception as e:  # "error reading hash from underlying"
+                    return "errors", e
+                if not under:
+                    return "no_hash", None
+                try:
+                    h = self.compute_hash(r, sources[r]())
+                except Exception as e:  # "error computing hash"
+                    return "errors", e
+                return ("differ", None) if h != under else ("ok", None)
+
+            def worker():
+                while True:
+                    with lock:
+                        r = next(it, None)
+                    if r is None:
+                        return
+                    kind, e = check_one(r)
+                    with lock:
+                        if kind == "errors":
+                            res["errors"][r] = e
+                        elif kind == "ok":
+                            res["ok"] += 1
+                        else:
+                            res[kind].append(r)
+
+            th = [threading.Thread(target=worker) for _ in range(checkers)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            res["differ"].sort()
+            res["no_hash"].sort()
+            return res
         for i in range(0, len(names), batch):
             part = names[i:i + batch]
             under, items, keep = {}, [], []

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "../../include/rclone_crypt_gpu.h"
+#include "md5_workers.h"
 #include "rc_internal.h"
 
 namespace rc {
@@ -363,7 +364,24 @@ struct rc_encrypter {
   int64_t buf_index = 0, buf_size = 0;
   int32_t err = RC_NIL;
   bool finished = false;
+  // crypt.put's tee hash (crypt.go:516-533) taken by the encrypter itself (rc_encrypter_set_md5):
+  // a worker hashes batch k while the consumer reads it and the next refill seals batch k+1 into
+  // the other wire buffer.  md5 covers every byte produced once `job` is done; md5_cur is the
+  // state before the batch being served (for a consumer that stops inside a batch).
+  bool md5_on = false;
+  bool wsel = false;  // md5_on: the batch being served is in wire2 (else wire)
+  PinnedBuf wire2;
+  xs::HostMd5 md5, md5_cur;
+  xs::Md5Job job;
 };
+
+// the bytes the encrypter is serving now: the header, then the current wire batch
+static const uint8_t* enc_cur(const rc_encrypter* fh) {
+  return fh->in_hdr ? fh->hdr : (fh->md5_on && fh->wsel ? fh->wire2.p : fh->wire.p);
+}
+
+// Batches below this are hashed on the stream's own thread (a worker hand-off costs ~10 us).
+constexpr int64_t kInlineMd5 = 256 << 10;
 
 // finish (cipher.go:748-758)
 static int64_t enc_finish(rc_encrypter* fh, int32_t err, int32_t* out_err) {
@@ -373,8 +391,10 @@ static int64_t enc_finish(rc_encrypter* fh, int32_t err, int32_t* out_err) {
   }
   fh->finished = true;
   fh->err = err;
+  xs::md5_workers().wait(&fh->job);  // the worker may still be reading a wire buffer
   fh->plain.release();
   fh->wire.release();
+  fh->wire2.release();
   *out_err = err;
   return 0;
 }
@@ -425,7 +445,8 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
     fh->in_hdr = false;
     const uint32_t batch = next_batch(fh->c, fh->grow);
     if (!fh->plain.ensure((size_t)fh->c->batch_blocks * kBlockData) ||
-        !fh->wire.ensure((size_t)fh->c->batch_blocks * kBlockSize))
+        !fh->wire.ensure((size_t)fh->c->batch_blocks * kBlockSize) ||
+        (fh->md5_on && !fh->wire2.ensure((size_t)fh->c->batch_blocks * kBlockSize)))
       return enc_finish(fh, RC_ERR_GPU, err);
     const auto t0 = std::chrono::steady_clock::now();
     int64_t total = 0;
@@ -447,22 +468,67 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
     if (nb == 0) return enc_finish(fh, first_err, err);
     fh->grow = grow_batch(fh->c, batch, total, std::chrono::steady_clock::now() - t0);
     if (!fh->eng) fh->eng = xs_pool_next(cipher_pool(fh->c));
-    if (!fh->eng ||
-        xs_engine_seal(fh->eng, fh->c->data_key, fh->nonce, 0, fh->plain.p, (uint64_t)total, fh->wire.p) != XS_OK)
+    // with the tee hash on, seal into the wire buffer that is neither served nor being hashed
+    const bool into2 = fh->md5_on && !fh->wsel;
+    uint8_t* out = into2 ? fh->wire2.p : fh->wire.p;
+    if (!fh->eng || xs_engine_seal(fh->eng, fh->c->data_key, fh->nonce, 0, fh->plain.p, (uint64_t)total, out) != XS_OK)
       return enc_finish(fh, RC_ERR_GPU, err);
     fh->buf_index = 0;
     fh->buf_size = total + (int64_t)nb * kBlockHdr;
     rc_nonce_add(fh->nonce, nb);  // nonce.increment() once per sealed block
+    if (fh->md5_on) {
+      auto& w = xs::md5_workers();
+      w.wait(&fh->job);  // the previous batch is hashed: md5 covers everything served so far
+      fh->md5_cur = fh->md5;
+      fh->wsel = into2;
+      fh->job.st = &fh->md5;
+      fh->job.p = out;
+      fh->job.n = (size_t)fh->buf_size;
+      if (fh->buf_size < kInlineMd5) fh->md5.update(out, (size_t)fh->buf_size);
+      else w.submit(&fh->job);
+    }
   }
   int64_t m = fh->buf_size - fh->buf_index;
   if (m > n) m = n;
-  memcpy(p, (fh->in_hdr ? fh->hdr : fh->wire.p) + fh->buf_index, (size_t)m);
+  memcpy(p, enc_cur(fh) + fh->buf_index, (size_t)m);
   fh->buf_index += m;
   return m;
 }
 
 extern "C" void rc_encrypter_nonce(const rc_encrypter* fh, uint8_t out[24]) { memcpy(out, fh->nonce, 24); }
-extern "C" void rc_encrypter_free(rc_encrypter* fh) { delete fh; }
+
+extern "C" int32_t rc_encrypter_set_md5(rc_encrypter* fh, int32_t on) {
+  if (!fh) return RC_ERR_INVALID;
+  std::lock_guard<std::mutex> g(fh->mu);
+  if (!fh->in_hdr || fh->buf_index != 0 || fh->finished) return RC_ERR_INVALID;  // before the first Read only
+  fh->md5_on = on != 0;
+  fh->md5 = xs::HostMd5();
+  fh->md5_cur = fh->md5;
+  if (fh->md5_on) fh->md5.update(fh->hdr, kFileHdr);  // the header is the first "batch" served
+  return RC_NIL;
+}
+
+extern "C" int32_t rc_encrypter_md5(rc_encrypter* fh, uint8_t out[16]) {
+  if (!fh || !out) return RC_ERR_INVALID;
+  std::lock_guard<std::mutex> g(fh->mu);
+  if (!fh->md5_on) return RC_ERR_INVALID;
+  xs::md5_workers().wait(&fh->job);
+  // MD5 of exactly the bytes returned so far, like the TeeReader: all produced bytes when the
+  // current batch is used up (always so after EOF), else the state before it plus its served part
+  xs::HostMd5 h = fh->md5;
+  if (fh->buf_index < fh->buf_size && !fh->finished) {
+    h = fh->md5_cur;
+    h.update(enc_cur(fh), (size_t)fh->buf_index);
+  }
+  h.final(out);
+  return RC_NIL;
+}
+
+extern "C" void rc_encrypter_free(rc_encrypter* fh) {
+  if (!fh) return;
+  xs::md5_workers().wait(&fh->job);
+  delete fh;
+}
 
 // ---------------------------------------------------------------- decrypter
 struct rc_decrypter {
@@ -841,4 +907,85 @@ extern "C" int32_t rc_hash_batch_with_nonce(rc_cipher* c, uint64_t n, const rc_r
     return RC_ERR_GPU;
   for (size_t k = 0; k < idx.size(); k++) memcpy(md5 + 16 * idx[k], dig.data() + 16 * k, 16);
   return RC_NIL;
+}
+
+// ---------------------------------------------------------------- computeHashWithNonce, one object
+// computeHashWithNonce (crypt.go:784-806) as an unchanged caller runs it: one object per call, from
+// cryptcheck's --checkers goroutines (cmd/cryptcheck/cryptcheck.go:91-114) or bisync's check.  The
+// object is read in ReadFills of one block, as newEncrypter would, up to hash_batch_blocks() blocks
+// per GPU seal (concurrent callers' seals are group-committed by the engine).  The MD5 of
+// "RCLONE\0\0" || nonce || wire blocks runs on a host core: with a handful of objects in flight a
+// core is ~10x a GPU lane (one dependency chain per stream).  A worker hashes
+// batch k while this thread reads and seals batch k+1 into the other wire buffer.
+static uint32_t hash_batch_blocks() {
+  static const uint32_t v = [] {
+    const char* e = getenv("RCLONE_AMD_HASH_BLOCKS");
+    const int k = e ? atoi(e) : 16;
+    return (uint32_t)std::max(1, std::min(256, k));
+  }();
+  return v;
+}
+
+extern "C" int32_t rc_compute_hash_with_nonce(rc_cipher* c, rc_reader src, const uint8_t nonce[24], uint8_t md5[16]) {
+  if (!c || !src.read || !nonce || !md5) return RC_ERR_INVALID;
+  const uint32_t batch = hash_batch_blocks();
+  auto& w = xs::md5_workers();
+  xs::HostMd5 m;
+  m.update(kMagic, 8);
+  m.update(nonce, 24);
+  uint8_t n[24];
+  memcpy(n, nonce, 24);
+  PinnedBuf plain, wire[2];
+  xs::Md5Job job;
+  job.st = &m;
+  xs_engine* eng = nullptr;
+  int32_t err = RC_NIL;
+  for (int k = 0;; k ^= 1) {
+    if (!plain.ensure((size_t)batch * kBlockData) || !wire[k].ensure((size_t)batch * kBlockSize)) {
+      err = RC_ERR_GPU;
+      break;
+    }
+    int64_t total = 0;
+    uint32_t nb = 0;
+    bool end = false, short_read = false;
+    int32_t e = RC_NIL;
+    for (; nb < batch; nb++) {
+      const int64_t got = read_fill(src, plain.p + (int64_t)nb * kBlockData, kBlockData, &e);
+      if (got == 0) {  // encrypter.Read: n == 0 -> finish(err); io.Copy ends (EOF = success)
+        end = true;
+        break;
+      }
+      total += got;
+      if (got < kBlockData || e != RC_NIL) {  // the next ReadFill must be a fresh call
+        nb++;
+        short_read = true;
+        break;
+      }
+    }
+    if (nb > 0) {
+      if (!eng) eng = xs_pool_next(cipher_pool(c));
+      if (!eng || xs_engine_seal(eng, c->data_key, n, 0, plain.p, (uint64_t)total, wire[k].p) != XS_OK) {
+        err = RC_ERR_GPU;
+        break;
+      }
+      rc_nonce_add(n, nb);
+      w.wait(&job);  // batch k-1 hashed (its buffer is the one sealed into next)
+      job.p = wire[k].p;
+      job.n = (size_t)(total + (int64_t)nb * kBlockHdr);
+      // the stream's (probably) last batch is hashed here: nothing is left to overlap it with
+      if (end || short_read || (int64_t)job.n < kInlineMd5) m.update(job.p, job.n);
+      else w.submit(&job);
+    }
+    if (end) {
+      err = e == RC_EOF ? RC_NIL : e;
+      break;
+    }
+  }
+  w.wait(&job);
+  if (src.close) {  // defer fs.CheckClose(in, &err)
+    const int32_t ce = src.close(src.user);
+    if (err == RC_NIL && ce != RC_NIL) err = ce;
+  }
+  if (err == RC_NIL) m.final(md5);
+  return err;
 }

@@ -1,0 +1,97 @@
+// md5_workers.h -- host worker threads for the per-object ciphertext MD5 of the streaming paths:
+// crypt.put's tee hash (backend/crypt/crypt.go:516-533) and computeHashWithNonce's io.Copy into
+// the hasher (crypt.go:799-803), which unchanged callers run one object at a time per goroutine
+// (--transfers / --checkers).  MD5 is one dependency chain per stream, so a stream can only be
+// sped up by overlapping its hashing with its other work: while a worker hashes batch k of a
+// stream, the stream's own thread reads and seals batch k+1 (the GPU seals it) or serves it to
+// the consumer.  Jobs of one stream are submitted one at a time (the stream waits for job k before
+// submitting job k+1), so a stream's bytes are hashed in order.
+#pragma once
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "xs_host_md5.h"
+
+namespace xs {
+
+struct Md5Job {
+  HostMd5* st = nullptr;
+  const uint8_t* p = nullptr;
+  size_t n = 0;
+  std::atomic<int> busy{0};  // 1 from submit until the worker has hashed the bytes
+};
+
+class Md5Workers {
+ public:
+  explicit Md5Workers(int max_threads) : max_(max_threads) {}
+  int max_threads() const { return max_; }
+  // j->st is updated with j->p[0:n] on a worker; the caller waits with wait() before touching
+  // j->st or reusing j->p.  With no workers (max_threads 0) the hash runs here.
+  void submit(Md5Job* j) {
+    if (max_ <= 0) {
+      j->st->update(j->p, j->n);
+      return;
+    }
+    j->busy.store(1, std::memory_order_relaxed);
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(j);
+    if ((int)th_.size() < max_ && idle_ == 0) th_.emplace_back([this] { run(); });
+    cv_.notify_one();
+  }
+  void wait(Md5Job* j) {
+    if (!j->busy.load(std::memory_order_acquire)) return;
+    for (int k = 0; k < 64; k++) {  // a job hashes ~1 MiB (~1 ms): spin only briefly
+      if (!j->busy.load(std::memory_order_acquire)) return;
+      std::this_thread::yield();
+    }
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return !j->busy.load(std::memory_order_acquire); });
+  }
+
+ private:
+  void run() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      idle_++;
+      cv_.wait(lk, [&] { return !q_.empty(); });
+      idle_--;
+      Md5Job* j = q_.front();
+      q_.pop_front();
+      lk.unlock();
+      j->st->update(j->p, j->n);
+      lk.lock();
+      j->busy.store(0, std::memory_order_release);
+      done_.notify_all();  // under mu_: a waiter checks busy under mu_ too, so no lost wake-up
+    }
+  }
+  const int max_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  std::deque<Md5Job*> q_;
+  std::vector<std::thread> th_;
+  int idle_ = 0;
+};
+
+// Process-wide workers (never destroyed: threads stay parked until exit).  XS_MD5_WORKERS sets
+// their number (0: every stream hashes on its own thread); default min(8, cores / 2).
+inline Md5Workers& md5_workers() {
+  static Md5Workers* w = [] {
+    int n;
+    if (const char* e = getenv("XS_MD5_WORKERS")) {
+      n = std::max(0, atoi(e));
+    } else {
+      const unsigned hc = std::thread::hardware_concurrency();
+      n = (int)std::max(1u, std::min(8u, hc ? hc / 2 : 1u));
+    }
+    return new Md5Workers(n);
+  }();
+  return *w;
+}
+
+}  // namespace xs

@@ -17,6 +17,7 @@
 //   * concurrency (meaningful under TSan): many encrypters/decrypters sharing one cipher on
 //     several threads, and one rc_names_run batch over 16 host threads.
 // Exit status 0 and a final "sanitize ok" line mean every check passed.
+#include <algorithm>
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
@@ -27,6 +28,7 @@
 #include <vector>
 
 #include "../../include/rclone_crypt_gpu.h"
+#include "../../rclone_amd/csrc/xs_host_md5.h"
 
 extern "C" {
 void orc_encrypt_file(uint8_t* out, const uint8_t* in, int64_t len, const uint8_t nonce0[24], const uint8_t key[32]);
@@ -90,6 +92,18 @@ static int32_t src_close(void* u) {
   return RC_NIL;
 }
 static rc_reader mk(Src* s) { return rc_reader{src_read, src_close, nullptr, s}; }
+// a source whose Close fails (fs.CheckClose must surface it when nothing else failed)
+static int32_t src_close_fail(void* u) {
+  ((Src*)u)->closes++;
+  return RC_USER_BASE + 9;
+}
+static std::vector<uint8_t> md5_of(const uint8_t* p, size_t n) {
+  xs::HostMd5 m;
+  m.update(p, n);
+  std::vector<uint8_t> d(16);
+  m.final(d.data());
+  return d;
+}
 
 // read a whole stream with varying read sizes; returns the final error
 static int32_t drain_enc(rc_encrypter* e, std::vector<uint8_t>& out) {
@@ -560,6 +574,98 @@ static void test_names(rc_cipher* c) {
   CHECK(errs[0] == RC_NIL && empty[0].empty(), "empty segment");
 }
 
+
+// ---------------------------------------------------------------- per-object hashes
+// computeHashWithNonce (crypt.go:784-806): MD5 of the crypt file newEncrypter(src, &nonce) would
+// produce, the source closed once, reader errors / close errors returned as io.Copy + CheckClose do
+static void test_hash_with_nonce(rc_cipher* c, const uint8_t key[32]) {
+  const size_t lens[] = {0, 1, 65535, 65536, 65537, 16 * 65536, 16 * 65536 + 1, 48 * 65536 + 3, 3000001};
+  for (size_t L : lens)
+    for (size_t ch : {(size_t)4096, (size_t)65537, (size_t)1 << 30}) {
+      std::vector<uint8_t> plain = rbytes(L), nonce = rbytes(24);
+      if (L == 3000001) memset(nonce.data(), 0xFF, 8);
+      Src s;
+      s.p = plain.data();
+      s.n = L;
+      s.chunk = ch;
+      uint8_t got[16];
+      const int32_t err = rc_compute_hash_with_nonce(c, mk(&s), nonce.data(), got);
+      const std::vector<uint8_t> f = oracle_file(plain, nonce.data(), key);
+      CHECK(err == RC_NIL && md5_of(f.data(), f.size()) == std::vector<uint8_t>(got, got + 16) && s.closes == 1,
+            "hash L=%zu chunk=%zu err=%d closes=%d", L, ch, err, s.closes);
+    }
+  const std::vector<uint8_t> plain = rbytes(3 * 1048576 + 77), nonce = rbytes(24);
+  for (int64_t q : {0L, 1L, 65536L, 65537L, 1048576L, 2500000L}) {  // reader error: returned, source closed
+    Src s;
+    s.p = plain.data();
+    s.n = plain.size();
+    s.fail_at = q;
+    uint8_t got[16];
+    const int32_t err = rc_compute_hash_with_nonce(c, mk(&s), nonce.data(), got);
+    CHECK(err == s.fail_err && s.closes == 1, "hash reader error at %ld: err %d closes %d", (long)q, err, s.closes);
+    Src t = s;  // read error and close error: the read error wins
+    t.pos = 0;
+    t.closes = 0;
+    const int32_t err2 = rc_compute_hash_with_nonce(c, rc_reader{src_read, src_close_fail, nullptr, &t}, nonce.data(), got);
+    CHECK(err2 == t.fail_err && t.closes == 1, "hash reader+close error at %ld: %d", (long)q, err2);
+  }
+  Src s;  // clean read, failing close: the close error
+  s.p = plain.data();
+  s.n = plain.size();
+  uint8_t got[16];
+  const int32_t err = rc_compute_hash_with_nonce(c, rc_reader{src_read, src_close_fail, nullptr, &s}, nonce.data(), got);
+  CHECK(err == RC_USER_BASE + 9 && s.closes == 1, "hash close error: %d", err);
+  Src n;  // no close function (io.NopCloser)
+  n.p = plain.data();
+  n.n = 100;
+  CHECK(rc_compute_hash_with_nonce(c, rc_reader{src_read, nullptr, nullptr, &n}, nonce.data(), got) == RC_NIL,
+        "hash without close");
+  CHECK(rc_compute_hash_with_nonce(nullptr, mk(&n), nonce.data(), got) == RC_ERR_INVALID, "hash null cipher");
+}
+
+// crypt.put's tee hash taken by the encrypter: MD5 of exactly the bytes read so far
+static void test_encrypter_md5(rc_cipher* c, const uint8_t key[32]) {
+  for (size_t L : {(size_t)0, (size_t)1, (size_t)65536, (size_t)65537, (size_t)(5 * 1048576 + 3), (size_t)(9 * 1048576)}) {
+    std::vector<uint8_t> plain = rbytes(L), nonce = rbytes(24);
+    const std::vector<uint8_t> f = oracle_file(plain, nonce.data(), key);
+    // stop points: nothing read, inside the header, header only, inside / at the end of a batch, all
+    std::vector<size_t> stops = {0, 5, 32, 33, f.size() / 2, f.size()};
+    for (size_t stop : stops) {
+      if (stop > f.size()) continue;
+      Src s;
+      s.p = plain.data();
+      s.n = L;
+      s.chunk = 65537;
+      int32_t err = 0;
+      rc_encrypter* e = rc_encrypt_data(c, mk(&s), nonce.data(), &err);
+      if (!e) {
+        CHECK(false, "encrypt_data");
+        continue;
+      }
+      uint8_t d[16];
+      CHECK(rc_encrypter_md5(e, d) == RC_ERR_INVALID, "md5 while off");
+      CHECK(rc_encrypter_set_md5(e, 1) == RC_NIL, "set_md5");
+      std::vector<uint8_t> ct;
+      while (ct.size() < stop) {
+        uint8_t buf[70000];
+        const int64_t want = (int64_t)std::min<size_t>(sizeof buf, stop - ct.size());
+        const int64_t k = rc_encrypter_read(e, buf, want, &err);
+        ct.insert(ct.end(), buf, buf + k);
+        if (err != RC_NIL) break;
+      }
+      if (stop == f.size()) {  // the consumer also sees EOF (io.ReadAll)
+        uint8_t one;
+        CHECK(rc_encrypter_read(e, &one, 1, &err) == 0 && err == RC_EOF, "EOF after the stream");
+      }
+      CHECK(rc_encrypter_md5(e, d) == RC_NIL && ct.size() == stop &&
+                std::vector<uint8_t>(d, d + 16) == md5_of(f.data(), stop),
+            "encrypter md5 L=%zu stop=%zu got %zu", L, stop, ct.size());
+      CHECK(rc_encrypter_set_md5(e, 1) == (stop ? RC_ERR_INVALID : RC_NIL), "set_md5 after a read");
+      rc_encrypter_free(e);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- concurrency (TSan)
 static void test_concurrency(rc_cipher* c, const uint8_t key[32]) {
   std::atomic<int> bad{0};
@@ -594,6 +700,29 @@ static void test_concurrency(rc_cipher* c, const uint8_t key[32]) {
         std::vector<uint8_t> pt;
         if (drain_dec(h, pt) != RC_EOF || pt != plain) bad++;
         rc_decrypter_free(h);
+        // per-object hash (cryptcheck's checkers) and the encrypter's own tee hash (put's transfers),
+        // objects large enough to go through the MD5 workers
+        std::vector<uint8_t> big((size_t)(2 * 1048576 + t * 65536 + k * 1000 + 5), (uint8_t)(k + t));
+        const std::vector<uint8_t> bf = oracle_file(big, nonce, key), want = md5_of(bf.data(), bf.size());
+        Src b;
+        b.p = big.data();
+        b.n = big.size();
+        uint8_t hd[16];
+        if (rc_compute_hash_with_nonce(c, mk(&b), nonce, hd) != RC_NIL || std::vector<uint8_t>(hd, hd + 16) != want) bad++;
+        Src b2;
+        b2.p = big.data();
+        b2.n = big.size();
+        rc_encrypter* e2 = rc_encrypt_data(c, mk(&b2), nonce, &err);
+        if (!e2 || rc_encrypter_set_md5(e2, 1) != RC_NIL) {
+          bad++;
+          if (e2) rc_encrypter_free(e2);
+          continue;
+        }
+        std::vector<uint8_t> ct2;
+        if (drain_enc(e2, ct2) != RC_EOF || ct2 != bf || rc_encrypter_md5(e2, hd) != RC_NIL ||
+            std::vector<uint8_t>(hd, hd + 16) != want)
+          bad++;
+        rc_encrypter_free(e2);
       }
     });
   for (auto& t : th) t.join();
@@ -633,6 +762,8 @@ int main(int argc, char** argv) {
     test_round_trips(c, key);
     test_damaged(c, key);
     test_reader_errors(c, key);
+    test_hash_with_nonce(c, key);
+    test_encrypter_md5(c, key);
     test_seek_grid(c, key);
     test_names(c);
   }

@@ -41,10 +41,15 @@ def test_config1_copy_then_cryptcheck(sodium_vectors):
     assert all(fs.size(k) == cfg["size"] for k in plains)
     res = fs.cryptcheck({k: (lambda v=v: Buffer(v)) for k, v in plains.items()})
     assert res == {"differ": [], "no_hash": [], "errors": {}, "ok": n}
+    # the unchanged cryptcheck's shape: 8 checkers, one per-object ComputeHash each
+    res = fs.cryptcheck({k: (lambda v=v: Buffer(v)) for k, v in plains.items()}, checkers=8)
+    assert res == {"differ": [], "no_hash": [], "errors": {}, "ok": n}
     # a changed source file is reported as differing, and only it
     bad = dict(plains)
     bad["file0042"] = bad["file0042"][:-1] + bytes([bad["file0042"][-1] ^ 1])
     res = fs.cryptcheck({k: (lambda v=v: Buffer(v)) for k, v in bad.items()}, batch=300)
+    assert res["differ"] == ["file0042"] and res["ok"] == n - 1 and not res["errors"]
+    res = fs.cryptcheck({k: (lambda v=v: Buffer(v)) for k, v in bad.items()}, checkers=8)
     assert res["differ"] == ["file0042"] and res["ok"] == n - 1 and not res["errors"]
 
 

@@ -204,10 +204,13 @@ def test_e2e_sync_harness_small():
     exe = os.path.join(root, "tools", "e2e_sync")
     if not os.path.exists(exe):
         pytest.skip("tools/e2e_sync not built")
-    for mode in ("batch", "stream"):
+    shapes = [("batch", "encrypter", "batch"), ("stream", "encrypter", "stream"), ("stream", "reader", "batch")]
+    for k, (mode, tee, check) in enumerate(shapes):
         r = subprocess.run([exe, "--gib", "0.25", "--mode", mode, "--transfers", "8", "--group-mib", "64",
-                            "--dir", "/tmp/rc_e2e_test_%d_%s" % (os.getpid(), mode)],
+                            "--tee", tee, "--check-mode", check, "--checkers", "8",
+                            "--dir", "/tmp/rc_e2e_test_%d_%d" % (os.getpid(), k)],
                            capture_output=True, text=True, timeout=100)
         assert r.returncode == 0, r.stdout + r.stderr
         res = json.loads(r.stdout.strip().splitlines()[-1])
         assert res["ok"] and res["cryptcheck_differences"] == 0 and res["corruption_flagged"] == 1
+        assert res["put_hash_mismatches"] == 0 and res["check_mode"] == check

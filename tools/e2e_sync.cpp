@@ -13,13 +13,20 @@
 //            file on the GPU (the hash crypt.put tees off the ciphertext), the wire bodies D2H
 //            straight into the memory remote's (pinned) arena.  Two lanes (two engines) overlap
 //            one group's file reads and PCIe with the other's.
-//            stream mode (--mode stream) -- the reference's per-object shape: --transfers
-//            threads each run rc_encrypt_data over the open file (GPU behind the encrypter,
-//            cross-caller coalescing) and tee an MD5 of the ciphertext on the CPU.
+//            stream mode (--mode stream) -- the reference's per-object shape (an unchanged
+//            fs/sync + crypt.put): --transfers threads each run rc_encrypt_data over the open file
+//            (GPU behind the encrypter, cross-caller coalescing) and the memory remote's Put reads
+//            the stream into the object's buffer.  The tee MD5 of the ciphertext is taken by the
+//            encrypter (rc_encrypter_set_md5, host workers; --tee encrypter, the default) or by
+//            the reading thread (--tee reader, crypt.go:516-533's TeeReader as is).
 //            Either way crypt.put then compares the tee hash with the remote's Object.Hash
 //            (CPU MD5 of the stored bytes, cached) unless --check-dst-hash 0.
-//   check  : cryptcheck -- every local file re-sealed with the nonce read back from the stored
-//            header and MD5'd on the GPU (xs_engine_seal_md5), compared with the remote's hash.
+//   check  : cryptcheck, batch (--check-mode batch, default) -- every local file re-sealed with the
+//            nonce read back from the stored header and MD5'd on the GPU (xs_engine_seal_md5),
+//            compared with the remote's hash; stream (--check-mode stream) -- the unchanged
+//            cmd/cryptcheck's shape (cryptcheck.go:91-114): --checkers threads, each per object
+//            reading the nonce through newDecrypter over the header (rc_decrypt_data) and calling
+//            computeHashWithNonce (rc_compute_hash_with_nonce) on the open local file.
 //   verify : sampled objects decrypted back through rc_decrypt_data (GPU) and compared with the
 //            local bytes; one stored object corrupted -> cryptcheck must flag exactly that one.
 // Prints one JSON line.
@@ -30,6 +37,7 @@
 //   devices: --devices 0,1,... puts lane l's engine on device list[l % n] and the rc_* handles
 //            and name engines on the same list (RCLONE_AMD_DEVICES): one process over several GPUs.
 //   usage: e2e_sync [--gib G] [--dir D] [--transfers T] [--mode batch|stream]
+//                   [--tee encrypter|reader] [--check-mode batch|stream] [--checkers C]
 //                   [--check-dst-hash 0|1] [--group-mib M] [--lanes L] [--keep]
 //                   [--anchor FILE] [--devices LIST]
 #include <fcntl.h>
@@ -310,9 +318,9 @@ static bool names_batch(rc_cipher* c, int32_t op, const std::vector<const std::s
 int main(int argc, char** argv) {
   double gib = 8.0;
   std::string dir = "/tmp/rc_e2e_src", mode = "batch";
-  int transfers = 16, check_dst = 1, keep = 0, nlanes = 4;
+  int transfers = 16, check_dst = 1, keep = 0, nlanes = 4, checkers = 8;
   uint64_t group_mib = 4096;
-  std::string anchor, devices;
+  std::string anchor, devices, tee_mode = "encrypter", check_mode = "batch";
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
     auto nx = [&] { return std::string(i + 1 < argc ? argv[++i] : ""); };
@@ -326,12 +334,17 @@ int main(int argc, char** argv) {
     else if (a == "--lanes") nlanes = std::max(1, atoi(nx().c_str()));
     else if (a == "--anchor") anchor = nx();
     else if (a == "--devices") devices = nx();
+    else if (a == "--tee") tee_mode = nx();
+    else if (a == "--check-mode") check_mode = nx();
+    else if (a == "--checkers") checkers = std::max(1, atoi(nx().c_str()));
     else {
       fprintf(stderr, "unknown argument %s\n", a.c_str());
       return 2;
     }
   }
   if (mode != "batch" && mode != "stream") return 2;
+  if (tee_mode != "encrypter" && tee_mode != "reader") return 2;
+  if (check_mode != "batch" && check_mode != "stream") return 2;
   std::vector<int> devs;
   if (!devices.empty()) {
     setenv("RCLONE_AMD_DEVICES", devices.c_str(), 1);  // rc_* handles and name engines
@@ -436,7 +449,8 @@ int main(int argc, char** argv) {
     memcpy(objs[i].header, kMagic, 8);
     memcpy(objs[i].header + 8, nonces.data() + 24 * i, 24);
   }
-  const int lanes = nlanes;
+  // lanes (engine + pinned group staging) serve the batch shapes only
+  const int lanes = (mode == "batch" || check_mode == "batch") ? nlanes : 0;
   std::vector<xs_engine*> eng(lanes);
   std::vector<uint8_t*> stage(lanes);
   for (int l = 0; l < lanes; l++) {
@@ -505,6 +519,7 @@ int main(int argc, char** argv) {
     sync_read = t_read;
     sync_gpu = t_gpu;
   } else {
+    const bool tee_on_enc = tee_mode == "encrypter";
     const double t0 = now();
     parallel_for(objs.size(), transfers, [&](size_t i) {
       Obj& o = objs[i];
@@ -516,28 +531,39 @@ int main(int argc, char** argv) {
       rc_reader r{fd_read, nullptr, nullptr, &fr};  // the encrypter does not close its source
       int32_t e = 0;
       rc_encrypter* h = rc_encrypt_data(c, r, nonces.data() + 24 * i, &e);
-      if (!h) {
+      if (!h || (tee_on_enc && rc_encrypter_set_md5(h, 1) != RC_NIL)) {
         failures++;
+        if (h) rc_encrypter_free(h);
+        fd_close(&fr);
         return;
       }
-      // memory backend Put reads the stream into its buffer; crypt.put tees the MD5
+      // the memory backend's Put reads the stream into the object's buffer (io.ReadAll): header,
+      // then the wire body straight into the remote's arena; crypt.put tees the MD5 of what it
+      // read -- in the encrypter, or here on the reading thread (TeeReader)
       Md5 tee;
-      std::vector<uint8_t> ct(32 + o.body_len + 1);
       uint64_t got = 0;
+      const uint64_t want = 32 + o.body_len;
       for (;;) {
-        const int64_t k = rc_encrypter_read(h, ct.data() + got, (int64_t)(ct.size() - got), &e);
+        uint8_t* dst = got < 32 ? o.header + got : o.body + (got - 32);
+        const uint64_t room = got < 32 ? 32 - got : want - got;
+        uint8_t probe;  // past the end: the read that returns EOF
+        const int64_t k = rc_encrypter_read(h, room ? dst : &probe, room ? (int64_t)std::min<uint64_t>(room, 1 << 20) : 1, &e);
+        if (k > 0 && !room) {
+          got = want + 1;  // longer than the object: a failure
+          break;
+        }
+        if (!tee_on_enc && k > 0) tee.update(dst, (size_t)k);
         got += (uint64_t)k;
-        if (e != RC_NIL || got == ct.size()) break;
+        if (e != RC_NIL) break;
       }
+      if (tee_on_enc) e = e == RC_EOF && rc_encrypter_md5(h, o.tee) == RC_NIL ? RC_EOF : RC_ERR_INVALID;
+      else tee.final(o.tee);
       rc_encrypter_free(h);
-      if ((e != RC_EOF && e != RC_NIL) || got != 32 + o.body_len) {
+      fd_close(&fr);
+      if (e != RC_EOF || got != want || memcmp(o.header, kMagic, 8) || memcmp(o.header + 8, nonces.data() + 24 * i, 24)) {
         failures++;
         return;
       }
-      tee.update(ct.data(), got);
-      tee.final(o.tee);
-      memcpy(o.body, ct.data() + 32, o.body_len);
-      fd_close(&fr);
     });
     t_sync = now() - t0 + t_names_enc;
   }
@@ -554,6 +580,37 @@ int main(int argc, char** argv) {
   // ---- cryptcheck: re-seal each local file with the stored nonce, MD5 on the GPU, compare
   auto cryptcheck = [&](std::vector<uint8_t>& differ) {
     differ.assign(objs.size(), 0);
+    if (check_mode == "stream") {  // cmd/cryptcheck as is: --checkers goroutines, one object each
+      parallel_for(objs.size(), checkers, [&](size_t i) {
+        Obj& o = objs[i];
+        dst_hash(o);  // underlyingDst.Hash (memory.go:580-588; cached by put's check)
+        // ComputeHash (crypt.go:816-852): open the stored object's header range, newDecrypter
+        // reads the nonce, close; then computeHashWithNonce over the opened source
+        MemReader hr{o.header, 32, nullptr, 0, 0};
+        int32_t e = 0;
+        rc_decrypter* d = rc_decrypt_data(c, rc_reader{mem_read, mem_close, nullptr, &hr}, &e);
+        if (!d) {
+          failures++;
+          return;
+        }
+        uint8_t nonce[24], md5[16];
+        rc_decrypter_nonce(d, nonce);
+        e = rc_decrypter_close(d);
+        rc_decrypter_free(d);
+        FdReader fr{open(o.name.c_str(), O_RDONLY)};
+        if (e != RC_NIL || fr.fd < 0) {
+          failures++;
+          if (fr.fd >= 0) close(fr.fd);
+          return;
+        }
+        if (rc_compute_hash_with_nonce(c, rc_reader{fd_read, fd_close, nullptr, &fr}, nonce, md5) != RC_NIL) {
+          failures++;
+          return;
+        }
+        differ[i] = memcmp(md5, o.dst, 16) != 0;
+      });
+      return;
+    }
     run_groups([&](int l, size_t g, const std::vector<uint64_t>& offs) {
       const size_t a = groups[g].first, n = groups[g].second - a;
       std::vector<uint8_t> ns(24 * n), md5(16 * n);
@@ -654,6 +711,7 @@ int main(int argc, char** argv) {
   const bool ok = failures == 0 && put_mismatch == 0 && ndiff == 0 && verify_bad == 0 && only_victim && name_mismatch == 0;
   const double g = (double)total / 1073741824.0;
   printf("{\"config\": \"configs[4] e2e: sync local tree -> crypt(memory), cryptcheck\", \"mode\": \"%s\", "
+         "\"tee\": \"%s\", \"check_mode\": \"%s\", \"checkers\": %d, "
          "\"objects\": %zu, \"gib\": %.3f, \"transfers\": %d, \"lanes\": %d, \"group_mib\": %llu, "
          "\"sync_s\": %.3f, \"sync_GiB_s\": %.2f, \"dst_hash_s\": %.3f, \"sync_with_hash_check_GiB_s\": %.2f, "
          "\"cryptcheck_s\": %.3f, \"cryptcheck_GiB_s\": %.2f, \"put_hash_mismatches\": %llu, "
@@ -662,7 +720,7 @@ int main(int argc, char** argv) {
          "\"name_mismatches\": %llu, \"example_remote_name\": \"%s\", "
          "\"anchored_objects\": %llu, \"devices\": \"%s\", \"tree_write_s\": %.2f, \"lane_seconds\": {\"sync_read\": %.3f, "
          "\"sync_gpu\": %.3f, \"check_read\": %.3f, \"check_gpu\": %.3f}, \"ok\": %s}\n",
-         mode.c_str(), objs.size(), g, transfers, lanes, (unsigned long long)group_mib, t_sync, g / t_sync, t_dst,
+         mode.c_str(), mode == "stream" ? tee_mode.c_str() : "gpu", check_mode.c_str(), checkers, objs.size(), g, transfers, lanes, (unsigned long long)group_mib, t_sync, g / t_sync, t_dst,
          check_dst ? g / (t_sync + t_dst) : 0.0, t_check, g / t_check, (unsigned long long)put_mismatch,
          (unsigned long long)ndiff, (unsigned long long)verified, (unsigned long long)verify_bad,
          (unsigned long long)flagged, t_names_enc, t_names_dec, (unsigned long long)name_mismatch,
