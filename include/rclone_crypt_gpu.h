@@ -209,7 +209,23 @@ int xs_pool_put_batch(xs_pool *p, const uint8_t key[32], uint64_t nobj, const ui
 
 /* Pinned (page-locked) host memory. */
 void *xs_host_alloc(size_t bytes);
+/* ... placed on NUMA node `node` (preferred-node policy during the allocation; node < 0: no
+ * preference).  Free with xs_host_free. */
+void *xs_host_alloc_node(size_t bytes, int node);
 void xs_host_free(void *p);
+
+/* Node topology (one process over a multi-socket 8-GPU node): each engine's
+ * pinned staging, its handles' staging and the host threads the library starts for it (host MD5,
+ * batched-call ranges) are placed on the NUMA node of the engine's GPU.  The sysfs root is
+ * RCLONE_AMD_SYSFS_ROOT (default /sys); RCLONE_AMD_NUMA=0 turns placement off. */
+int xs_device_numa_node(int device);          /* NUMA node of a HIP device's PCI function, or -1 */
+int xs_engine_numa_node(const xs_engine *e);  /* the node the engine's host resources use, or -1 */
+int xs_pci_numa_node(const char *pci_bus_id); /* <root>/bus/pci/devices/<id>/numa_node, or -1 */
+/* CPUs of a node (<root>/devices/system/node/node<N>/cpulist): writes up to cap, returns the count
+ * (0 when unknown). */
+int xs_numa_node_cpus(int node, int *cpus, int cap);
+/* Parse a device list as RCLONE_AMD_DEVICES ("0,1,1,2": repeats allowed); returns the count. */
+int xs_parse_device_list(const char *list, int *out, int cap);
 
 /* ------------------------------------------------------------------------------------
  * rc_*: backend/crypt/cipher.go data API.
@@ -308,6 +324,12 @@ rc_decrypter *rc_decrypt_data(rc_cipher *c, rc_reader rc, int32_t *err);
 /* DecryptDataSeek (:1112) */
 rc_decrypter *rc_decrypt_data_seek(rc_cipher *c, rc_open_fn open, void *open_user, int64_t offset,
                                    int64_t limit, int32_t *err);
+/* DecryptDataSeek with the wrapped error: when *err is RC_ERR_REOPEN (or RC_ERR_SHORT_NONCE) the
+ * handle is gone, and *wrapped receives the opener's own error -- the %w operand of "couldn't
+ * reopen file with offset and limit: %w" (cipher.go:1011) -- so the binding can wrap the real
+ * cause (errors.Is on context.Canceled, fs.ErrorObjectNotFound, ...).  wrapped may be NULL. */
+rc_decrypter *rc_decrypt_data_seek_ex(rc_cipher *c, rc_open_fn open, void *open_user, int64_t offset,
+                                      int64_t limit, int32_t *err, int32_t *wrapped);
 int64_t rc_decrypter_read(rc_decrypter *d, uint8_t *p, int64_t n, int32_t *err); /* :901 */
 int64_t rc_decrypter_range_seek(rc_decrypter *d, int64_t offset, int32_t whence, int64_t limit,
                                 int32_t *err);                                   /* :972 */

@@ -21,8 +21,11 @@ package gpucipher
 rc_reader gpucipher_reader(uintptr_t h, int closer, int range_seeker);
 rc_encrypter *gpucipher_encrypt(rc_cipher *c, uintptr_t in, const uint8_t *nonce, int32_t *err);
 rc_decrypter *gpucipher_decrypt(rc_cipher *c, uintptr_t rc, int range_seeker, int32_t *err);
-rc_decrypter *gpucipher_decrypt_seek(rc_cipher *c, uintptr_t open_state, int64_t offset, int64_t limit, int32_t *err);
-int32_t gpucipher_hash_batch(rc_cipher *c, uint64_t n, const uintptr_t *srcs, const uint8_t *nonces, uint8_t *md5, int32_t *errs);
+rc_decrypter *gpucipher_decrypt_seek(rc_cipher *c, uintptr_t open_state, int64_t offset, int64_t limit, int32_t *err,
+                                     int32_t *wrapped);
+int32_t gpucipher_compute_hash(rc_cipher *c, uintptr_t src, int closer, const uint8_t *nonce, uint8_t *md5);
+int32_t gpucipher_hash_batch(rc_cipher *c, uint64_t n, const uintptr_t *srcs, uint64_t n_nonces, const uint8_t *nonces,
+                             uint8_t *md5, int32_t *errs);
 */
 import "C"
 
@@ -60,7 +63,10 @@ func Register(tooShort, badHeader, badMagic, badBlock, closed, badSeek error) {
 }
 
 // errTable holds the Go errors produced by the readers / openers of one handle; C sees index
-// codes >= RC_USER_BASE.
+// codes >= RC_USER_BASE.  The library may return a code again and again (a finished stream's
+// sticky error, cipher.go:748-758 / :1042-1052), so entries stay for the handle's life; an error
+// value seen before gets its old code back, so the table grows only with distinct errors (a
+// reader that keeps failing the same way adds one entry, not one per call).
 type errTable struct {
 	mu   sync.Mutex
 	errs []error
@@ -77,8 +83,23 @@ func (t *errTable) code(err error) C.int32_t {
 	}
 	t.mu.Lock()
 	defer t.mu.Unlock()
+	for i := len(t.errs) - 1; i >= 0; i-- {
+		if sameError(t.errs[i], err) {
+			return C.int32_t(C.RC_USER_BASE + i)
+		}
+	}
 	t.errs = append(t.errs, err)
 	return C.int32_t(C.RC_USER_BASE + len(t.errs) - 1)
+}
+
+// sameError: the identical error value (== on comparable dynamic types; never panics).
+func sameError(a, b error) (same bool) {
+	defer func() {
+		if recover() != nil {
+			same = false
+		}
+	}()
+	return a == b
 }
 
 func (t *errTable) err(code C.int32_t) error {
@@ -123,10 +144,16 @@ func goRead(h C.uintptr_t, p *C.uint8_t, n C.int64_t, errp *C.int32_t) C.int64_t
 //export goClose
 func goClose(h C.uintptr_t) C.int32_t {
 	b := cgo.Handle(h).Value().(*readerBox)
+	code := C.int32_t(C.RC_NIL)
 	if c, ok := b.r.(io.Closer); ok {
-		return b.t.code(c.Close())
+		code = b.t.code(c.Close())
 	}
-	return C.RC_NIL
+	if b.s != nil {
+		// the library closes a reader once and never uses it again (Close, or RangeSeek
+		// replacing it, cipher.go:1004-1015): drop it now instead of at the decrypter's end
+		b.s.forget(cgo.Handle(h))
+	}
+	return code
 }
 
 //export goRangeSeek
@@ -153,16 +180,41 @@ type openState struct {
 	open    OpenRangeSeek
 	t       *errTable
 	mu      sync.Mutex
-	handles []cgo.Handle // readers handed to C, deleted when the decrypter is freed
+	handles map[cgo.Handle]struct{} // readers handed to C and not yet closed by it
 }
 
 func (s *openState) newReader(r io.Reader, closer bool) C.rc_reader {
 	hd := cgo.NewHandle(&readerBox{r: r, t: s.t, s: s})
 	s.mu.Lock()
-	s.handles = append(s.handles, hd)
+	if s.handles == nil {
+		s.handles = map[cgo.Handle]struct{}{}
+	}
+	s.handles[hd] = struct{}{}
 	s.mu.Unlock()
 	_, seeker := r.(fs.RangeSeeker)
 	return C.gpucipher_reader(C.uintptr_t(hd), cbool(closer), cbool(seeker))
+}
+
+// forget deletes a reader's handle once the library has closed it (each handle is deleted once).
+func (s *openState) forget(hd cgo.Handle) {
+	s.mu.Lock()
+	_, live := s.handles[hd]
+	delete(s.handles, hd)
+	s.mu.Unlock()
+	if live {
+		hd.Delete()
+	}
+}
+
+// release deletes every handle still held (idempotent).
+func (s *openState) release() {
+	s.mu.Lock()
+	hs := s.handles
+	s.handles = nil
+	s.mu.Unlock()
+	for hd := range hs {
+		hd.Delete()
+	}
 }
 
 //export goOpen
@@ -212,14 +264,44 @@ func New(dataKey, nameKey *[32]byte, nameTweak *[16]byte, passBadBlocks bool) (*
 	return c, nil
 }
 
+// ComputeHashWithNonce is computeHashWithNonce (crypt.go:784-806) for MD5: src (already opened,
+// as crypt.go opens it) is read to EOF, sealed with nonce on the GPU -- concurrent checkers'
+// seals share launches -- and "RCLONE\0\0" || nonce || wire blocks is MD5'd on host cores; src is
+// closed when it is an io.Closer (defer fs.CheckClose(in, &err)).  The only change crypt.go needs:
+//
+//	if f.cipher.gpu != nil && hashType == hash.MD5 {
+//		sum, err := f.cipher.gpu.ComputeHashWithNonce((*[24]byte)(&nonce), in)
+//		if err != nil {
+//			return "", fmt.Errorf("failed to hash data: %w", err)
+//		}
+//		return hex.EncodeToString(sum[:]), nil
+//	}
+func (c *Cipher) ComputeHashWithNonce(nonce *[24]byte, src io.Reader) (sum [16]byte, err error) {
+	t := &errTable{}
+	hd := cgo.NewHandle(&readerBox{r: src, t: t})
+	defer hd.Delete()
+	_, closer := src.(io.Closer)
+	rc := C.gpucipher_compute_hash(c.h, C.uintptr_t(hd), cbool(closer), (*C.uint8_t)(unsafe.Pointer(&nonce[0])),
+		(*C.uint8_t)(unsafe.Pointer(&sum[0])))
+	runtime.KeepAlive(c)
+	if rc != C.RC_NIL {
+		if rc == C.RC_ERR_GPU {
+			return sum, fmt.Errorf("gpucipher: %s", C.GoString(C.xs_last_error()))
+		}
+		return sum, t.err(rc)
+	}
+	return sum, nil
+}
+
 // ---------------------------------------------------------------------------- encrypter
 
 // Encrypter is an io.Reader of the encrypted stream (cipher.go:681 encrypter).
 type Encrypter struct {
-	c  *Cipher
-	h  *C.rc_encrypter
-	t  *errTable
-	hd cgo.Handle
+	c    *Cipher
+	h    *C.rc_encrypter
+	t    *errTable
+	hd   cgo.Handle
+	done sync.Once // hd deleted: the stream has finished and the library reads its source no more
 }
 
 // NewEncrypter is newEncrypter(in, nonce) (cipher.go:694).  The nonce must be given: the
@@ -237,9 +319,33 @@ func (c *Cipher) NewEncrypter(in io.Reader, nonce *[24]byte) (*Encrypter, error)
 	fh := &Encrypter{c: c, h: h, t: t, hd: hd}
 	runtime.SetFinalizer(fh, func(fh *Encrypter) {
 		C.rc_encrypter_free(fh.h)
-		fh.hd.Delete()
+		fh.release()
 	})
 	return fh, nil
+}
+
+func (fh *Encrypter) release() { fh.done.Do(fh.hd.Delete) }
+
+// SetMD5 makes the encrypter take crypt.put's ciphertext hash itself (crypt.go:516-533), hashed
+// on host workers while the wrapped Put reads; call it before the first Read.  put then skips its
+// TeeReader and uses MD5() as srcHash.
+func (fh *Encrypter) SetMD5() error {
+	rc := C.rc_encrypter_set_md5(fh.h, 1)
+	runtime.KeepAlive(fh)
+	if rc != C.RC_NIL {
+		return errors.New("gpucipher: SetMD5 after the first Read")
+	}
+	return nil
+}
+
+// MD5 is the MD5 of exactly the bytes Read has returned (hasher.Sums() of the TeeReader).
+func (fh *Encrypter) MD5() (sum [16]byte, err error) {
+	rc := C.rc_encrypter_md5(fh.h, (*C.uint8_t)(unsafe.Pointer(&sum[0])))
+	runtime.KeepAlive(fh)
+	if rc != C.RC_NIL {
+		return sum, errors.New("gpucipher: MD5 without SetMD5")
+	}
+	return sum, nil
 }
 
 // Read as per io.Reader (cipher.go:719): the library copies into p and never retains it.
@@ -249,8 +355,14 @@ func (fh *Encrypter) Read(p []byte) (int, error) {
 	}
 	var e C.int32_t
 	n := C.rc_encrypter_read(fh.h, (*C.uint8_t)(unsafe.Pointer(&p[0])), C.int64_t(len(p)), &e)
+	err := fh.t.err(e)
+	if err != nil {
+		// finish (cipher.go:748-758): the stream is over, the library never reads the source
+		// again -- drop its handle now rather than when the finalizer runs
+		fh.release()
+	}
 	runtime.KeepAlive(fh)
-	return int(n), fh.t.err(e)
+	return int(n), err
 }
 
 // Nonce is fh.nonce: the initial nonce before the first Read, the next block's after.
@@ -265,30 +377,31 @@ func (fh *Encrypter) Nonce() (n [24]byte) {
 // Decrypter is io.ReadCloser + io.Seeker + fs.RangeSeeker of plaintext (cipher.go:776
 // decrypter, :69-74 ReadSeekCloser).
 type Decrypter struct {
-	c  *Cipher
-	h  *C.rc_decrypter
-	s  *openState
-	hd cgo.Handle // of s (DecryptDataSeek only)
+	c    *Cipher
+	h    *C.rc_decrypter
+	s    *openState
+	hd   cgo.Handle // of s (DecryptDataSeek only)
+	done sync.Once  // Go handles released (Close, or the finalizer as a backstop)
 }
 
 func (c *Cipher) newDecrypter(s *openState, h *C.rc_decrypter, hd cgo.Handle) *Decrypter {
 	fh := &Decrypter{c: c, h: h, s: s, hd: hd}
 	runtime.SetFinalizer(fh, func(fh *Decrypter) {
 		C.rc_decrypter_free(fh.h)
-		for _, x := range fh.s.handles {
-			x.Delete()
-		}
-		if fh.hd != 0 {
-			fh.hd.Delete()
-		}
+		fh.release()
 	})
 	return fh
 }
 
-func (s *openState) release() {
-	for _, x := range s.handles {
-		x.Delete()
-	}
+// release drops the reader and opener handles.  Once closed the library calls none of them:
+// Read, Seek and RangeSeek return ErrorFileClosed (cipher.go:1069-1087).
+func (fh *Decrypter) release() {
+	fh.done.Do(func() {
+		fh.s.release()
+		if fh.hd != 0 {
+			fh.hd.Delete()
+		}
+	})
 }
 
 // DecryptData is newDecrypter(rc) (cipher.go:793, :1099).
@@ -310,12 +423,15 @@ func (c *Cipher) DecryptData(rc io.ReadCloser) (*Decrypter, error) {
 func (c *Cipher) DecryptDataSeek(ctx context.Context, open OpenRangeSeek, offset, limit int64) (*Decrypter, error) {
 	s := &openState{ctx: ctx, open: open, t: &errTable{}}
 	hd := cgo.NewHandle(s)
-	var e C.int32_t
-	h := C.gpucipher_decrypt_seek(c.h, C.uintptr_t(hd), C.int64_t(offset), C.int64_t(limit), &e)
+	var e, w C.int32_t
+	h := C.gpucipher_decrypt_seek(c.h, C.uintptr_t(hd), C.int64_t(offset), C.int64_t(limit), &e, &w)
+	runtime.KeepAlive(c)
 	if h == nil {
 		err := s.t.err(e)
 		if e == C.RC_ERR_REOPEN || e == C.RC_ERR_SHORT_NONCE {
-			err = wrap(e, err)
+			// the opener's own error, wrapped with %w as cipher.go:1011 does, so errors.Is /
+			// fserrors.Cause still see context.Canceled, fs.ErrorObjectNotFound, ...
+			err = wrap(e, s.t.err(w))
 		}
 		s.release()
 		hd.Delete()
@@ -370,9 +486,12 @@ func (fh *Decrypter) Seek(offset int64, whence int) (int64, error) {
 	return fh.RangeSeek(context.TODO(), offset, whence, -1)
 }
 
-// Close (cipher.go:1069): closes the underlying reader once; ErrorFileClosed afterwards.
+// Close (cipher.go:1069): closes the underlying reader once; ErrorFileClosed afterwards.  The
+// reader and opener handles are released here (idempotently); the finalizer only frees the
+// library handle, and releases the Go handles of a Decrypter that was never closed.
 func (fh *Decrypter) Close() error {
 	err := fh.toErr(C.rc_decrypter_close(fh.h))
+	fh.release()
 	runtime.KeepAlive(fh)
 	return err
 }
@@ -391,6 +510,10 @@ func (fh *Decrypter) Nonce() (n [24]byte) {
 // MD5'd on the GPU.  errs[i] is the reference's "failed to hash data: %w" for a failing source.
 func (c *Cipher) HashBatchWithNonce(nonces [][24]byte, srcs []io.ReadCloser) (sums [][16]byte, errs []error, err error) {
 	n := len(srcs)
+	if len(nonces) != n {
+		// fewer nonces would hash sources with zero nonces and report false differences
+		return nil, nil, fmt.Errorf("gpucipher: %d nonces for %d sources", len(nonces), n)
+	}
 	if n == 0 {
 		return nil, nil, nil
 	}
@@ -413,8 +536,10 @@ func (c *Cipher) HashBatchWithNonce(nonces [][24]byte, srcs []io.ReadCloser) (su
 	}
 	md5 := make([]byte, 16*n)
 	codes := make([]C.int32_t, n)
-	if rc := C.gpucipher_hash_batch(c.h, C.uint64_t(n), &handles[0], (*C.uint8_t)(unsafe.Pointer(&flat[0])),
-		(*C.uint8_t)(unsafe.Pointer(&md5[0])), &codes[0]); rc != C.RC_NIL {
+	rc := C.gpucipher_hash_batch(c.h, C.uint64_t(n), &handles[0], C.uint64_t(len(nonces)),
+		(*C.uint8_t)(unsafe.Pointer(&flat[0])), (*C.uint8_t)(unsafe.Pointer(&md5[0])), &codes[0])
+	runtime.KeepAlive(c) // the finalizer must not free c.h while the batch runs
+	if rc != C.RC_NIL {
 		return nil, nil, fmt.Errorf("gpucipher: %s", C.GoString(C.xs_last_error()))
 	}
 	sums, errs = make([][16]byte, n), make([]error, n)

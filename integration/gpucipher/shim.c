@@ -43,15 +43,24 @@ rc_decrypter *gpucipher_decrypt(rc_cipher *c, uintptr_t rc, int range_seeker, in
   return rc_decrypt_data(c, gpucipher_reader(rc, 1, range_seeker), err);
 }
 
-/* DecryptDataSeek (cipher.go:1112): open_state is the handle of the Go OpenRangeSeek */
+/* DecryptDataSeek (cipher.go:1112): open_state is the handle of the Go OpenRangeSeek; *wrapped gets
+ * the opener's error behind RC_ERR_REOPEN (the %w operand, cipher.go:1011) */
 rc_decrypter *gpucipher_decrypt_seek(rc_cipher *c, uintptr_t open_state, int64_t offset, int64_t limit,
-                                     int32_t *err) {
-  return rc_decrypt_data_seek(c, shim_open, (void *)open_state, offset, limit, err);
+                                     int32_t *err, int32_t *wrapped) {
+  return rc_decrypt_data_seek_ex(c, shim_open, (void *)open_state, offset, limit, err, wrapped);
 }
 
-/* computeHashWithNonce (crypt.go:784) batched: srcs[i] handles of io.Readers, closed after use */
-int32_t gpucipher_hash_batch(rc_cipher *c, uint64_t n, const uintptr_t *srcs, const uint8_t *nonces, uint8_t *md5,
-                             int32_t *errs) {
+/* computeHashWithNonce (crypt.go:784), one object: src is the handle of an io.Reader, closed after
+ * use when it is an io.Closer (closer != 0) */
+int32_t gpucipher_compute_hash(rc_cipher *c, uintptr_t src, int closer, const uint8_t *nonce, uint8_t *md5) {
+  return rc_compute_hash_with_nonce(c, gpucipher_reader(src, closer, 0), nonce, md5);
+}
+
+/* computeHashWithNonce (crypt.go:784) batched: srcs[i] handles of io.Readers, closed after use.
+ * n_nonces is len(nonces) on the Go side: a mismatch is refused before any source is read. */
+int32_t gpucipher_hash_batch(rc_cipher *c, uint64_t n, const uintptr_t *srcs, uint64_t n_nonces,
+                             const uint8_t *nonces, uint8_t *md5, int32_t *errs) {
+  if (n_nonces != n) return RC_ERR_INVALID;
   rc_reader *r = (rc_reader *)malloc((n ? n : 1) * sizeof *r);
   if (!r) return RC_ERR_INVALID;
   for (uint64_t i = 0; i < n; i++) r[i] = gpucipher_reader(srcs[i], 1, 0);

@@ -78,6 +78,12 @@ _SIGS = [
     ("xs_pool_seal_md5", ctypes.c_int, [vp, ctypes.c_char_p, u64, vp, vp, vp, vp, vp]),
     ("xs_pool_put_batch", ctypes.c_int, [vp, ctypes.c_char_p, u64, vp, vp, vp, vp, vp, vp]),
     ("xs_host_alloc", vp, [ctypes.c_size_t]),
+    ("xs_host_alloc_node", vp, [ctypes.c_size_t, ctypes.c_int]),
+    ("xs_device_numa_node", ctypes.c_int, [ctypes.c_int]),
+    ("xs_engine_numa_node", ctypes.c_int, [vp]),
+    ("xs_pci_numa_node", ctypes.c_int, [ctypes.c_char_p]),
+    ("xs_numa_node_cpus", ctypes.c_int, [ctypes.c_int, vp, ctypes.c_int]),
+    ("xs_parse_device_list", ctypes.c_int, [ctypes.c_char_p, vp, ctypes.c_int]),
     ("xs_host_free", None, [vp]),
     # cipher.go mirror
     ("rc_cipher_new", vp, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(i32)]),
@@ -105,6 +111,7 @@ _SIGS = [
     ("rc_encrypter_md5", i32, [vp, vp]),
     ("rc_decrypt_data", vp, [vp, RcReader, ctypes.POINTER(i32)]),
     ("rc_decrypt_data_seek", vp, [vp, OPEN_FN, vp, i64, i64, ctypes.POINTER(i32)]),
+    ("rc_decrypt_data_seek_ex", vp, [vp, OPEN_FN, vp, i64, i64, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
     ("rc_decrypter_read", i64, [vp, vp, i64, ctypes.POINTER(i32)]),
     ("rc_decrypter_range_seek", i64, [vp, i64, i32, i64, ctypes.POINTER(i32)]),
     ("rc_decrypter_close", i32, [vp]),

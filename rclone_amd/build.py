@@ -14,7 +14,8 @@ LIB = os.path.join(HERE, "librclone_crypt.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RCLONE_AMD_ARCH", "gfx950")
 
-SOURCES = ["xs_kernels.hip", "xs_md5.hip", "xs_eme.hip", "xs_probe.hip", "xs_api.cpp", "cipher.cpp", "names.cpp", "names_gpu.cpp", "scrypt.cpp"]
+SOURCES = ["xs_kernels.hip", "xs_md5.hip", "xs_eme.hip", "xs_probe.hip", "xs_api.cpp", "xs_topo.cpp", "cipher.cpp", "names.cpp",
+           "names_gpu.cpp", "scrypt.cpp"]
 
 
 # what the crypt kernels (xs_seal / xs_open / keygen) are compiled from: PMC counters committed under
@@ -44,7 +45,7 @@ def needs_build():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = sources() + [os.path.join(CSRC, h) for h in ("xs_internal.h", "xs_aes.h", "rc_internal.h", "xs_host_md5.h", "md5_workers.h")] + [
+    deps = sources() + [os.path.join(CSRC, h) for h in ("xs_internal.h", "xs_aes.h", "rc_internal.h", "xs_host_md5.h", "md5_workers.h", "xs_topo.h")] + [
                         os.path.join(os.path.dirname(HERE), "include", "rclone_crypt_gpu.h")]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 

@@ -109,9 +109,11 @@ class _ErrTable:
             return CryptError("can't seek - not initialised with newDecrypterSeek")
         if code == -109:
             return CryptError("can only seek from the start")
-        if code == -110:
+        if code == -110:  # fmt.Errorf("couldn't reopen file with offset and limit: %w", err)
             inner = self.exc(wrapped) if wrapped not in (None, RC_NIL) else CryptError("?")
-            return CryptError(f"couldn't reopen file with offset and limit: {inner}")
+            e = CryptError(f"couldn't reopen file with offset and limit: {inner}")
+            e.__cause__ = inner
+            return e
         cls = _CODE_TO_CLASS.get(code)
         if cls is not None:
             return cls(cls.message)
@@ -504,7 +506,11 @@ class Decrypter:
                 except Exception as ex:
                     return _ERRS.code(ex)
             self._open_cb = _lib.OPEN_FN(_open)
-            self._h = _lib.lib().rc_decrypt_data_seek(cipher._h, self._open_cb, None, offset, limit, ctypes.byref(e))
+            w = ctypes.c_int32(0)
+            self._h = _lib.lib().rc_decrypt_data_seek_ex(cipher._h, self._open_cb, None, offset, limit, ctypes.byref(e),
+                                                         ctypes.byref(w))
+            if not self._h:
+                _raise(e.value, wrapped=w.value)  # RC_ERR_REOPEN: the opener's own error as the cause
         if not self._h:
             _raise(e.value)
             raise GPUError(GPUError.message)

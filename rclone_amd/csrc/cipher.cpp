@@ -96,38 +96,52 @@ namespace {
 
 // Pinned staging pool -- the counterpart of the reference's Cipher.buffers sync.Pool
 // (cipher.go:179, :255-262): handles come and go per object, and hipHostMalloc/hipHostFree
-// cost milliseconds and synchronise the device, so buffers are recycled (best fit by size),
-// keeping at most kPoolBytes cached.
+// cost milliseconds and synchronise the device, so buffers are recycled (best fit by size, per
+// NUMA node: a handle's staging sits on the node of its engine's GPU), keeping at most
+// kPoolBytes cached.
 constexpr size_t kPoolBytes = (size_t)1 << 30;
 std::mutex g_pool_mu;
 // process-lifetime cache, deliberately never destroyed: buffers stay reachable (no exit-time
 // hipHostFree after the HIP runtime may already be torn down)
-std::multimap<size_t, uint8_t*>& g_pool = *new std::multimap<size_t, uint8_t*>();
+std::map<int, std::multimap<size_t, uint8_t*>>& g_pool = *new std::map<int, std::multimap<size_t, uint8_t*>>();
 size_t g_pool_cached = 0;
 
-uint8_t* pool_get(size_t bytes, size_t* cap) {
+// Page-locked when possible.  If pinning fails (no device, pinned-memory limit) the buffer is plain
+// heap memory: a source that fails before its first block never needs the GPU, and the engine
+// stages pageable buffers through its own copies.
+uint8_t* pool_get(size_t bytes, size_t* cap, int node, bool* heap) {
+  *heap = false;
   {
     std::lock_guard<std::mutex> g(g_pool_mu);
-    auto it = g_pool.lower_bound(bytes);
-    if (it != g_pool.end() && it->first <= 2 * bytes + (1u << 20)) {
+    auto& m = g_pool[node];
+    auto it = m.lower_bound(bytes);
+    if (it != m.end() && it->first <= 2 * bytes + (1u << 20)) {
       *cap = it->first;
       uint8_t* p = it->second;
       g_pool_cached -= it->first;
-      g_pool.erase(it);
+      m.erase(it);
       return p;
     }
   }
-  uint8_t* p = (uint8_t*)xs_host_alloc(bytes);
+  uint8_t* p = (uint8_t*)xs_host_alloc_node(bytes, node);
+  if (!p) {
+    p = (uint8_t*)aligned_alloc(64, (bytes + 63) & ~(size_t)63);
+    *heap = p != nullptr;
+  }
   *cap = p ? bytes : 0;
   return p;
 }
 
-void pool_put(uint8_t* p, size_t cap) {
+void pool_put(uint8_t* p, size_t cap, int node, bool heap) {
   if (!p) return;
+  if (heap) {
+    free(p);
+    return;
+  }
   {
     std::lock_guard<std::mutex> g(g_pool_mu);
     if (g_pool_cached + cap <= kPoolBytes) {
-      g_pool.emplace(cap, p);
+      g_pool[node].emplace(cap, p);
       g_pool_cached += cap;
       return;
     }
@@ -138,10 +152,14 @@ void pool_put(uint8_t* p, size_t cap) {
 struct PinnedBuf {
   uint8_t* p = nullptr;
   size_t n = 0;
-  bool ensure(size_t bytes) {
-    if (n >= bytes) return true;
-    pool_put(p, n);
-    p = pool_get(bytes, &n);
+  int node = -1;      // NUMA node of p (the owner's engine's)
+  bool heap = false;  // pinning failed: plain heap memory
+  // at least `bytes` on node `want_node` (contents dropped)
+  bool ensure(size_t bytes, int want_node = -1) {
+    if (n >= bytes && node == want_node) return true;
+    pool_put(p, n, node, heap);
+    node = want_node;
+    p = pool_get(bytes, &n, node, &heap);
     return p != nullptr;
   }
   // grow keeping the contents (doubling)
@@ -150,18 +168,21 @@ struct PinnedBuf {
     size_t want = n ? n : (1u << 20);
     while (want < bytes) want *= 2;
     size_t cap = 0;
-    uint8_t* q = pool_get(want, &cap);
+    bool qheap = false;
+    uint8_t* q = pool_get(want, &cap, node, &qheap);
     if (!q) return false;
     if (p) memcpy(q, p, n);
-    pool_put(p, n);
+    pool_put(p, n, node, heap);
     p = q;
     n = cap;
+    heap = qheap;
     return true;
   }
   void release() {
-    pool_put(p, n);
+    pool_put(p, n, node, heap);
     p = nullptr;
     n = 0;
+    heap = false;
   }
   ~PinnedBuf() { release(); }
 };
@@ -391,7 +412,7 @@ static int64_t enc_finish(rc_encrypter* fh, int32_t err, int32_t* out_err) {
   }
   fh->finished = true;
   fh->err = err;
-  xs::md5_workers().wait(&fh->job);  // the worker may still be reading a wire buffer
+  xs::md5_wait(&fh->job);  // the worker may still be reading a wire buffer
   fh->plain.release();
   fh->wire.release();
   fh->wire2.release();
@@ -444,9 +465,12 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
     // refill: ReadFill block by block exactly as encrypter.Read would, up to next_batch blocks
     fh->in_hdr = false;
     const uint32_t batch = next_batch(fh->c, fh->grow);
-    if (!fh->plain.ensure((size_t)fh->c->batch_blocks * kBlockData) ||
-        !fh->wire.ensure((size_t)fh->c->batch_blocks * kBlockSize) ||
-        (fh->md5_on && !fh->wire2.ensure((size_t)fh->c->batch_blocks * kBlockSize)))
+    if (!fh->eng) fh->eng = xs_pool_next(cipher_pool(fh->c));  // staging goes on its GPU's node
+    if (!fh->eng) return enc_finish(fh, RC_ERR_GPU, err);
+    const int node = xs_engine_numa_node(fh->eng);
+    if (!fh->plain.ensure((size_t)fh->c->batch_blocks * kBlockData, node) ||
+        !fh->wire.ensure((size_t)fh->c->batch_blocks * kBlockSize, node) ||
+        (fh->md5_on && !fh->wire2.ensure((size_t)fh->c->batch_blocks * kBlockSize, node)))
       return enc_finish(fh, RC_ERR_GPU, err);
     const auto t0 = std::chrono::steady_clock::now();
     int64_t total = 0;
@@ -467,17 +491,16 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
     }
     if (nb == 0) return enc_finish(fh, first_err, err);
     fh->grow = grow_batch(fh->c, batch, total, std::chrono::steady_clock::now() - t0);
-    if (!fh->eng) fh->eng = xs_pool_next(cipher_pool(fh->c));
     // with the tee hash on, seal into the wire buffer that is neither served nor being hashed
     const bool into2 = fh->md5_on && !fh->wsel;
     uint8_t* out = into2 ? fh->wire2.p : fh->wire.p;
-    if (!fh->eng || xs_engine_seal(fh->eng, fh->c->data_key, fh->nonce, 0, fh->plain.p, (uint64_t)total, out) != XS_OK)
+    if (xs_engine_seal(fh->eng, fh->c->data_key, fh->nonce, 0, fh->plain.p, (uint64_t)total, out) != XS_OK)
       return enc_finish(fh, RC_ERR_GPU, err);
     fh->buf_index = 0;
     fh->buf_size = total + (int64_t)nb * kBlockHdr;
     rc_nonce_add(fh->nonce, nb);  // nonce.increment() once per sealed block
     if (fh->md5_on) {
-      auto& w = xs::md5_workers();
+      auto& w = xs::md5_workers(node);
       w.wait(&fh->job);  // the previous batch is hashed: md5 covers everything served so far
       fh->md5_cur = fh->md5;
       fh->wsel = into2;
@@ -512,7 +535,7 @@ extern "C" int32_t rc_encrypter_md5(rc_encrypter* fh, uint8_t out[16]) {
   if (!fh || !out) return RC_ERR_INVALID;
   std::lock_guard<std::mutex> g(fh->mu);
   if (!fh->md5_on) return RC_ERR_INVALID;
-  xs::md5_workers().wait(&fh->job);
+  xs::md5_wait(&fh->job);
   // MD5 of exactly the bytes returned so far, like the TeeReader: all produced bytes when the
   // current batch is used up (always so after EOF), else the state before it plus its served part
   xs::HostMd5 h = fh->md5;
@@ -526,7 +549,7 @@ extern "C" int32_t rc_encrypter_md5(rc_encrypter* fh, uint8_t out[16]) {
 
 extern "C" void rc_encrypter_free(rc_encrypter* fh) {
   if (!fh) return;
-  xs::md5_workers().wait(&fh->job);
+  xs::md5_wait(&fh->job);
   delete fh;
 }
 
@@ -560,9 +583,12 @@ struct rc_decrypter {
 // staging for a full batch, allocated when the first block is read (not at open: a header
 // error or a failing source never needs it)
 static bool dec_alloc(rc_decrypter* fh) {
+  if (!fh->eng) fh->eng = xs_pool_next(cipher_pool(fh->c));  // staging goes on its GPU's node
+  if (!fh->eng) return false;
   const uint32_t batch = fh->c->batch_blocks;
-  return fh->wire.ensure((size_t)batch * kBlockSize) && fh->plain.ensure((size_t)batch * kBlockData) &&
-         fh->okb.ensure(batch);
+  const int node = xs_engine_numa_node(fh->eng);
+  return fh->wire.ensure((size_t)batch * kBlockSize, node) && fh->plain.ensure((size_t)batch * kBlockData, node) &&
+         fh->okb.ensure(batch, node);
 }
 
 // finish (cipher.go:1042-1052): sets the sticky error and returns it
@@ -633,8 +659,7 @@ static int32_t dec_read_batch(rc_decrypter* fh, uint32_t want) {
   fh->nblk = nb;
   if (nb == 0) return RC_NIL;
   fh->grow = grow_batch(fh->c, ra, total, std::chrono::steady_clock::now() - t0);
-  if (!fh->eng) fh->eng = xs_pool_next(cipher_pool(fh->c));
-  if (!fh->eng || xs_engine_open(fh->eng, fh->c->data_key, fh->nonce, 0, fh->wire.p, (uint64_t)total, fh->plain.p,
+  if (xs_engine_open(fh->eng, fh->c->data_key, fh->nonce, 0, fh->wire.p, (uint64_t)total, fh->plain.p,
                                  fh->okb.p) != XS_OK) {
     fh->nblk = 0;
     return RC_ERR_GPU;
@@ -714,6 +739,12 @@ static int64_t range_seek_locked(rc_decrypter* fh, int64_t offset, int32_t whenc
 
 extern "C" rc_decrypter* rc_decrypt_data_seek(rc_cipher* c, rc_open_fn open, void* open_user, int64_t offset,
                                               int64_t limit, int32_t* err) {
+  return rc_decrypt_data_seek_ex(c, open, open_user, offset, limit, err, nullptr);
+}
+
+extern "C" rc_decrypter* rc_decrypt_data_seek_ex(rc_cipher* c, rc_open_fn open, void* open_user, int64_t offset,
+                                                 int64_t limit, int32_t* err, int32_t* wrapped) {
+  if (wrapped) *wrapped = RC_NIL;
   if (!c || !open) {
     if (err) *err = RC_ERR_INVALID;
     return nullptr;
@@ -747,6 +778,8 @@ extern "C" rc_decrypter* rc_decrypt_data_seek(rc_cipher* c, rc_open_fn open, voi
     int32_t se = RC_NIL;
     range_seek_locked(fh, offset, 0, limit, &se);
     if (se != RC_NIL) {
+      // the %w operand of "couldn't reopen file with offset and limit: %w" (cipher.go:1011)
+      if (wrapped && (se == RC_ERR_REOPEN || se == RC_ERR_SHORT_NONCE)) *wrapped = fh->wrapped;
       dec_close_locked(fh);  // fh.Close()
       delete fh;
       if (err) *err = se;
@@ -869,8 +902,6 @@ extern "C" int32_t rc_hash_batch_with_nonce(rc_cipher* c, uint64_t n, const rc_r
                                             uint8_t* md5, int32_t* errs) {
   if (n == 0) return RC_NIL;
   if (!c || !srcs || !nonces || !md5 || !errs) return RC_ERR_INVALID;
-  xs_pool* pool = cipher_pool(c);
-  if (!pool) return RC_ERR_GPU;
   PinnedBuf buf;
   uint64_t pos = 0;
   std::vector<uint64_t> offs, lens;
@@ -901,7 +932,9 @@ extern "C" int32_t rc_hash_batch_with_nonce(rc_cipher* c, uint64_t n, const rc_r
     ns.insert(ns.end(), nonces + 24 * i, nonces + 24 * i + 24);
     idx.push_back(i);
   }
-  if (idx.empty()) return RC_NIL;
+  if (idx.empty()) return RC_NIL;  // every source failed: nothing for the GPU
+  xs_pool* pool = cipher_pool(c);
+  if (!pool) return RC_ERR_GPU;
   std::vector<uint8_t> dig(16 * idx.size());
   if (xs_pool_seal_md5(pool, c->data_key, idx.size(), ns.data(), offs.data(), lens.data(), buf.p, dig.data()) != XS_OK)
     return RC_ERR_GPU;
@@ -929,7 +962,9 @@ static uint32_t hash_batch_blocks() {
 extern "C" int32_t rc_compute_hash_with_nonce(rc_cipher* c, rc_reader src, const uint8_t nonce[24], uint8_t md5[16]) {
   if (!c || !src.read || !nonce || !md5) return RC_ERR_INVALID;
   const uint32_t batch = hash_batch_blocks();
-  auto& w = xs::md5_workers();
+  xs_engine* eng = xs_pool_next(cipher_pool(c));
+  const int node = eng ? xs_engine_numa_node(eng) : -1;
+  auto& w = xs::md5_workers(node);
   xs::HostMd5 m;
   m.update(kMagic, 8);
   m.update(nonce, 24);
@@ -938,10 +973,9 @@ extern "C" int32_t rc_compute_hash_with_nonce(rc_cipher* c, rc_reader src, const
   PinnedBuf plain, wire[2];
   xs::Md5Job job;
   job.st = &m;
-  xs_engine* eng = nullptr;
   int32_t err = RC_NIL;
   for (int k = 0;; k ^= 1) {
-    if (!plain.ensure((size_t)batch * kBlockData) || !wire[k].ensure((size_t)batch * kBlockSize)) {
+    if (!plain.ensure((size_t)batch * kBlockData, node) || !wire[k].ensure((size_t)batch * kBlockSize, node)) {
       err = RC_ERR_GPU;
       break;
     }
@@ -963,7 +997,6 @@ extern "C" int32_t rc_compute_hash_with_nonce(rc_cipher* c, rc_reader src, const
       }
     }
     if (nb > 0) {
-      if (!eng) eng = xs_pool_next(cipher_pool(c));
       if (!eng || xs_engine_seal(eng, c->data_key, n, 0, plain.p, (uint64_t)total, wire[k].p) != XS_OK) {
         err = RC_ERR_GPU;
         break;

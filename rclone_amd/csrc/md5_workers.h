@@ -16,20 +16,23 @@
 #include <thread>
 #include <vector>
 
+#include "rc_internal.h"
 #include "xs_host_md5.h"
 
 namespace xs {
 
+class Md5Workers;
 struct Md5Job {
   HostMd5* st = nullptr;
   const uint8_t* p = nullptr;
   size_t n = 0;
   std::atomic<int> busy{0};  // 1 from submit until the worker has hashed the bytes
+  const Md5Workers* owner = nullptr;
 };
 
 class Md5Workers {
  public:
-  explicit Md5Workers(int max_threads) : max_(max_threads) {}
+  Md5Workers(int max_threads, int node) : max_(max_threads), node_(node) {}
   int max_threads() const { return max_; }
   // j->st is updated with j->p[0:n] on a worker; the caller waits with wait() before touching
   // j->st or reusing j->p.  With no workers (max_threads 0) the hash runs here.
@@ -38,13 +41,18 @@ class Md5Workers {
       j->st->update(j->p, j->n);
       return;
     }
+    j->owner = this;
     j->busy.store(1, std::memory_order_relaxed);
     std::lock_guard<std::mutex> g(mu_);
     q_.push_back(j);
-    if ((int)th_.size() < max_ && idle_ == 0) th_.emplace_back([this] { run(); });
+    if ((int)th_.size() < max_ && idle_ == 0)
+      th_.emplace_back([this] {
+        pin_thread_to_node(node_);  // the node of the engines whose streams it hashes
+        run();
+      });
     cv_.notify_one();
   }
-  void wait(Md5Job* j) {
+  void wait(Md5Job* j) const {
     if (!j->busy.load(std::memory_order_acquire)) return;
     for (int k = 0; k < 64; k++) {  // a job hashes ~1 MiB (~1 ms): spin only briefly
       if (!j->busy.load(std::memory_order_acquire)) return;
@@ -70,18 +78,24 @@ class Md5Workers {
       done_.notify_all();  // under mu_: a waiter checks busy under mu_ too, so no lost wake-up
     }
   }
-  const int max_;
-  std::mutex mu_;
-  std::condition_variable cv_, done_;
+  const int max_, node_;
+  mutable std::mutex mu_;
+  mutable std::condition_variable cv_, done_;
   std::deque<Md5Job*> q_;
   std::vector<std::thread> th_;
   int idle_ = 0;
 };
 
-// Process-wide workers (never destroyed: threads stay parked until exit).  XS_MD5_WORKERS sets
-// their number (0: every stream hashes on its own thread); default min(8, cores / 2).
-inline Md5Workers& md5_workers() {
-  static Md5Workers* w = [] {
+// Process-wide workers, one set per NUMA node (never destroyed: threads stay parked until exit).
+// XS_MD5_WORKERS sets their number per node (0: every stream hashes on its own thread); default
+// min(8, cores / 2).
+inline Md5Workers& md5_workers(int node) {
+  constexpr int kNodes = 64;
+  static std::mutex mu;
+  static Md5Workers* w[kNodes + 1] = {nullptr};
+  const int slot = node >= 0 && node < kNodes ? node + 1 : 0;
+  std::lock_guard<std::mutex> g(mu);
+  if (!w[slot]) {
     int n;
     if (const char* e = getenv("XS_MD5_WORKERS")) {
       n = std::max(0, atoi(e));
@@ -89,9 +103,15 @@ inline Md5Workers& md5_workers() {
       const unsigned hc = std::thread::hardware_concurrency();
       n = (int)std::max(1u, std::min(8u, hc ? hc / 2 : 1u));
     }
-    return new Md5Workers(n);
-  }();
-  return *w;
+    w[slot] = new Md5Workers(n, slot - 1);
+  }
+  return *w[slot];
+}
+
+// Wait for a job submitted to any node's workers (no-op for an idle job).
+inline void md5_wait(Md5Job* j) {
+  if (!j->busy.load(std::memory_order_acquire)) return;
+  j->owner->wait(j);
 }
 
 }  // namespace xs

@@ -7,12 +7,15 @@
 
 #include "../../include/rclone_crypt_gpu.h"
 #include "xs_aes.h"
+#include "xs_topo.h"
 
 namespace xs {
 void set_error(const char* fmt, ...);  // thread-local message returned by xs_last_error
 // Devices a process spreads its work over: RCLONE_AMD_DEVICES ("0,1,2,3"; repeats allowed),
-// else RCLONE_AMD_DEVICE, else every visible device.
+// else RCLONE_AMD_DEVICE, else the local rank's device when LOCAL_RANK is set (one process per
+// GPU), else every visible device.
 std::vector<int> default_devices();
+
 }  // namespace xs
 
 struct rc_cipher {

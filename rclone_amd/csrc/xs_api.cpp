@@ -24,6 +24,7 @@
 
 #include "xs_host_md5.h"
 #include "xs_internal.h"
+#include "xs_topo.h"
 
 namespace xs {
 static thread_local std::string g_err;
@@ -292,15 +293,39 @@ int xs_fill_blocks_dev(void* d, uint64_t nblocks, uint64_t first_block, uint64_t
   return XS_OK;
 }
 
-void* xs_host_alloc(size_t bytes) {
+void* xs_host_alloc_node(size_t bytes, int node) {
   void* p = nullptr;
-  const hipError_t e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable);
+  hipError_t e = hipErrorUnknown;
+  if (node >= 0 && numa_enabled()) {
+    // the pages follow the calling thread's policy (hipHostMallocNumaUser), preferred = node
+    xs::ScopedMemPolicy pol(node);
+    e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable | hipHostMallocNumaUser);
+    if (e != hipSuccess) (void)hipGetLastError();
+  }
+  if (e != hipSuccess) e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable);
   if (e != hipSuccess) {
     set_error("hipHostMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
     return nullptr;
   }
   xs::pin_register(p, bytes ? bytes : 1);
   return p;
+}
+
+void* xs_host_alloc(size_t bytes) { return xs_host_alloc_node(bytes, -1); }
+
+// NUMA node of a device's PCI function (sysfs), cached per device
+int xs_device_numa_node(int device) {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(device);
+  if (it != cache.end()) return it->second;
+  char bus[64] = {0};
+  int node = -1;
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, device) == hipSuccess) node = xs::pci_numa_node(bus);
+  else (void)hipGetLastError();
+  cache[device] = node;
+  return node;
 }
 
 void xs_host_free(void* p) {
@@ -314,6 +339,7 @@ void xs_host_free(void* p) {
 // ---------------------------------------------------------------- engine
 struct xs_engine {
   int device = 0;
+  int numa = -1;  // NUMA node of the device: the engine's pinned staging and host threads go there
   uint32_t batch = 0;
   std::mutex mu;
   struct Slot {
@@ -434,13 +460,14 @@ static bool grow(uint8_t** p, size_t* cap, size_t need) {
   return true;
 }
 
-static bool grow_pinned(uint8_t** p, size_t* cap, size_t need) {  // grow-only (x1.5), contents dropped
+static bool grow_pinned(uint8_t** p, size_t* cap, size_t need, int node) {  // grow-only (x1.5), contents dropped
   if (*cap >= need) return true;
-  (void)hipHostFree(*p);
+  xs_host_free(*p);
   *p = nullptr;
   *cap = 0;
   const size_t want = std::max(need, need / 2 * 3);
-  if (hipHostMalloc((void**)p, want ? want : 16, hipHostMallocPortable) != hipSuccess) return false;
+  *p = (uint8_t*)xs_host_alloc_node(want ? want : 16, node);
+  if (!*p) return false;
   *cap = want;
   return true;
 }
@@ -483,7 +510,7 @@ static void engine_free(xs_engine* e) {
     (void)hipStreamDestroy(e->hb.aux);
   }
   if (e->hb.ev_sealed) (void)hipEventDestroy(e->hb.ev_sealed);
-  for (auto* r : e->hb.route) (void)hipHostFree(r);
+  for (auto* r : e->hb.route) xs_host_free(r);
   delete e;
 }
 
@@ -496,6 +523,7 @@ extern "C" xs_engine* xs_engine_create(int device, uint32_t batch_blocks, int ns
   }
   xs_engine* e = new xs_engine();
   e->device = device;
+  e->numa = numa_enabled() ? xs_device_numa_node(device) : -1;
   e->batch = batch_blocks;
   if (hipSetDevice(device) != hipSuccess) {
     set_error("hipSetDevice(%d) failed", device);
@@ -575,6 +603,8 @@ extern "C" void xs_engine_stats(xs_engine* e, uint64_t out[3]) {
 }
 
 extern "C" void xs_engine_destroy(xs_engine* e) { engine_free(e); }
+
+extern "C" int xs_engine_numa_node(const xs_engine* e) { return e ? e->numa : -1; }
 
 static int engine_sync(xs_engine* e) {
   int rc = XS_OK;
@@ -1190,6 +1220,7 @@ struct HostMd5Pool {
   std::vector<std::thread> th;
   uint64_t bytes = 0, count = 0;
   int pending[2] = {0, 0};  // unfinished jobs per staging buffer
+  int node = -1;            // the engine's NUMA node: workers run on its CPUs
 
   void push(const Job& j, int max_threads) {
     std::lock_guard<std::mutex> g(mu);
@@ -1197,7 +1228,11 @@ struct HostMd5Pool {
     count++;
     if (j.tag >= 0) pending[j.tag]++;
     jobs.push_back(j);
-    if ((int)th.size() < max_threads && th.size() < jobs.size() - next) th.emplace_back([this] { work(); });
+    if ((int)th.size() < max_threads && th.size() < jobs.size() - next)
+      th.emplace_back([this] {
+        pin_thread_to_node(node);
+        work();
+      });
     cv.notify_one();
   }
   void work() {
@@ -1258,6 +1293,7 @@ static int seal_md5_impl(xs_engine* e, const uint8_t key[32], uint64_t nobj, con
   hipStream_t st = e->slots[0].s;
   auto& hb = e->hb;
   HostMd5Pool host;  // joined (every digest written) before this function returns
+  host.node = e->numa;
   // groups of whole objects, ~budget plaintext bytes each (MD5 is sequential per object)
   // large groups: the MD5 of a group takes as long as its largest object (one lane each)
   const uint64_t budget = std::max<uint64_t>((uint64_t)e->batch * XS_BLOCK_DATA * 16, 4096ull << 20);
@@ -1353,7 +1389,7 @@ static int seal_md5_impl(xs_engine* e, const uint8_t key[32], uint64_t nobj, con
         need += wlen[host_obj[k] - o0];
       }
       host.wait_tag(tag);
-      if (!grow_pinned(&hb.route[tag], &hb.route_cap[tag], need)) {
+      if (!grow_pinned(&hb.route[tag], &hb.route_cap[tag], need, e->numa)) {
         set_error("xs_engine_seal_md5: pinned staging of %llu bytes failed", (unsigned long long)need);
         return XS_ERR_NOMEM;
       }
@@ -1452,23 +1488,20 @@ namespace xs {
 std::vector<int> default_devices() {
   std::vector<int> v;
   const char* list = getenv("RCLONE_AMD_DEVICES");
-  if (list && *list) {
-    const char* p = list;
-    while (*p) {
-      char* end = nullptr;
-      const long d = strtol(p, &end, 10);
-      if (end == p) break;
-      v.push_back((int)d);
-      p = end;
-      while (*p == ',' || *p == ' ') p++;
-    }
-    if (!v.empty()) return v;
-  }
+  if (list && *list && parse_device_list(list, &v) > 0) return v;
   if (const char* one = getenv("RCLONE_AMD_DEVICE")) {
-    v.push_back(atoi(one));
+    v.assign(1, atoi(one));
     return v;
   }
   const int n = xs_device_count();
+  // one process per GPU (torch.distributed.run and the like export LOCAL_RANK): that rank's
+  // device only, not engines (~170 MB + 5 streams each) on every GPU from every rank
+  if (const char* lr = getenv("LOCAL_RANK")) {
+    if (*lr && n > 0) {
+      v.assign(1, atoi(lr) % n);
+      return v;
+    }
+  }
   for (int d = 0; d < n; d++) v.push_back(d);
   return v;
 }
@@ -1556,6 +1589,7 @@ static int pool_seal_md5(xs_pool* p, const uint8_t key[32], uint64_t nobj, const
     for (uint64_t i = a; i < b; i++) bpos += (body_bytes(lens[i]) + 15) & ~15ull;
     xs_engine* e = p->engines[(first + r) % p->engines.size()];
     th.emplace_back([&, r, a, b, rb, e] {
+      pin_thread_to_node(e->numa);
       rc[r] = seal_md5_impl(e, key, b - a, nonces + 24 * a, offs + a, lens + a, plain, md5 + 16 * a, rb,
                             e->host_md5_threads >= 0 ? e->host_md5_threads : per, nullptr);
       if (rc[r] != XS_OK) msg[r] = xs_last_error();

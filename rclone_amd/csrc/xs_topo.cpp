@@ -1,0 +1,163 @@
+// xs_topo.cpp -- node topology for the multi-GPU host path.
+//
+// One rclone process spreads its --transfers / --checkers streams over the node's GPUs
+// (fs/sync/sync.go:544 startTransfers hands objects to a goroutine pool; xs_pool hands each stream
+// an engine).  On a two-socket 8-GPU node half of the GPUs hang off each socket, so an engine's
+// host-side resources -- its pinned staging, the handles' staging buffers and the host threads
+// that hash or feed its objects -- belong on the NUMA node of the engine's GPU, or every byte
+// crosses the socket link twice.  This file holds the host-only part: the sysfs lookups (PCI bus
+// id -> NUMA node -> CPU list), the device-list parser, thread pinning and a scoped memory policy
+// for pinned allocations.  The HIP part (device -> PCI bus id) is in xs_api.cpp.
+//
+// The sysfs root is RCLONE_AMD_SYSFS_ROOT (default /sys) so tests can point it at a fake tree.
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <cctype>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rc_internal.h"
+
+namespace xs {
+
+static std::string sysfs_root() {
+  const char* r = getenv("RCLONE_AMD_SYSFS_ROOT");
+  return r && *r ? std::string(r) : std::string("/sys");
+}
+
+static bool read_line(const std::string& path, std::string* out) {
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return false;
+  char buf[4096];
+  const bool ok = fgets(buf, sizeof buf, f) != nullptr;
+  fclose(f);
+  if (!ok) return false;
+  out->assign(buf);
+  while (!out->empty() && isspace((unsigned char)out->back())) out->pop_back();
+  return true;
+}
+
+// "0000:C1:00.0" -> NUMA node from <root>/bus/pci/devices/0000:c1:00.0/numa_node; -1 if unknown
+// (no such file, or the kernel reports -1 on a single-node machine)
+int pci_numa_node(const char* busid) {
+  if (!busid || !*busid) return -1;
+  std::string id(busid);
+  for (auto& ch : id) ch = (char)tolower((unsigned char)ch);
+  std::string v;
+  if (!read_line(sysfs_root() + "/bus/pci/devices/" + id + "/numa_node", &v) || v.empty()) return -1;
+  char* end = nullptr;
+  const long n = strtol(v.c_str(), &end, 10);
+  if (end == v.c_str() || n < 0 || n > 4095) return -1;
+  return (int)n;
+}
+
+// Linux cpulist format: "0-15,32-47" (ranges and single ids, comma separated); false if malformed
+bool parse_cpulist(const char* s, std::vector<int>* out) {
+  out->clear();
+  if (!s) return false;
+  const char* p = s;
+  while (*p) {
+    while (*p == ' ' || *p == ',') p++;
+    if (!*p || *p == '\n') break;
+    char* end = nullptr;
+    const long a = strtol(p, &end, 10);
+    if (end == p || a < 0) return false;
+    long b = a;
+    p = end;
+    if (*p == '-') {
+      p++;
+      b = strtol(p, &end, 10);
+      if (end == p || b < a) return false;
+      p = end;
+    }
+    if (b - a > 65536) return false;
+    for (long c = a; c <= b; c++) out->push_back((int)c);
+    if (*p && *p != ',' && *p != '\n' && *p != ' ') return false;
+  }
+  return true;
+}
+
+bool node_cpus(int node, std::vector<int>* cpus) {
+  cpus->clear();
+  if (node < 0) return false;
+  std::string v;
+  if (!read_line(sysfs_root() + "/devices/system/node/node" + std::to_string(node) + "/cpulist", &v)) return false;
+  return parse_cpulist(v.c_str(), cpus) && !cpus->empty();
+}
+
+// "0,1,1,2" -> {0,1,1,2} (repeats allowed: several engines on one device); stops at the first
+// entry that is not a number.  Returns the count.
+int parse_device_list(const char* s, std::vector<int>* out) {
+  out->clear();
+  if (!s) return 0;
+  const char* p = s;
+  while (*p) {
+    while (*p == ',' || *p == ' ') p++;
+    if (!*p) break;
+    char* end = nullptr;
+    const long d = strtol(p, &end, 10);
+    if (end == p || d < 0) break;
+    out->push_back((int)d);
+    p = end;
+  }
+  return (int)out->size();
+}
+
+// Pin the calling thread to the CPUs of `node` (no-op when the node or its CPU list is unknown, or
+// RCLONE_AMD_NUMA=0).  Only threads this library starts are pinned -- never a caller's thread.
+void pin_thread_to_node(int node) {
+  if (!numa_enabled()) return;
+  std::vector<int> cpus;
+  if (!node_cpus(node, &cpus)) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : cpus)
+    if (c < CPU_SETSIZE) CPU_SET(c, &set);
+  (void)sched_setaffinity(0, sizeof set, &set);
+}
+
+bool numa_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("RCLONE_AMD_NUMA");
+    return v ? atoi(v) != 0 : true;
+  }();
+  return on;
+}
+
+// Preferred-node memory policy for the calling thread while in scope (pinned allocations made in
+// it land on `node`); restores the previous policy.  No-op for node < 0.
+ScopedMemPolicy::ScopedMemPolicy(int node) {
+  if (node < 0 || node >= 1024 || !numa_enabled()) return;
+  unsigned long mask[1024 / (8 * sizeof(unsigned long))] = {0};
+  if (syscall(SYS_get_mempolicy, &old_mode_, old_mask_, 1024ul, nullptr, 0ul) != 0) return;
+  mask[node / (8 * sizeof(unsigned long))] |= 1ul << (node % (8 * sizeof(unsigned long)));
+  const int kMpolPreferred = 1;
+  active_ = syscall(SYS_set_mempolicy, kMpolPreferred, mask, 1024ul) == 0;
+}
+
+ScopedMemPolicy::~ScopedMemPolicy() {
+  if (active_) (void)syscall(SYS_set_mempolicy, old_mode_, old_mask_, 1024ul);
+}
+
+}  // namespace xs
+
+extern "C" int xs_pci_numa_node(const char* pci_bus_id) { return xs::pci_numa_node(pci_bus_id); }
+
+extern "C" int xs_numa_node_cpus(int node, int* cpus, int cap) {
+  std::vector<int> v;
+  if (!xs::node_cpus(node, &v)) return 0;
+  for (int i = 0; i < cap && i < (int)v.size(); i++) cpus[i] = v[i];
+  return (int)v.size();
+}
+
+extern "C" int xs_parse_device_list(const char* list, int* out, int cap) {
+  std::vector<int> v;
+  xs::parse_device_list(list, &v);
+  for (int i = 0; i < cap && i < (int)v.size(); i++) out[i] = v[i];
+  return (int)v.size();
+}

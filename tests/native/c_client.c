@@ -19,7 +19,11 @@
 rc_reader gpucipher_reader(uintptr_t h, int closer, int range_seeker);
 rc_encrypter *gpucipher_encrypt(rc_cipher *c, uintptr_t in, const uint8_t *nonce, int32_t *err);
 rc_decrypter *gpucipher_decrypt(rc_cipher *c, uintptr_t rc, int range_seeker, int32_t *err);
-rc_decrypter *gpucipher_decrypt_seek(rc_cipher *c, uintptr_t open_state, int64_t offset, int64_t limit, int32_t *err);
+rc_decrypter *gpucipher_decrypt_seek(rc_cipher *c, uintptr_t open_state, int64_t offset, int64_t limit, int32_t *err,
+                                     int32_t *wrapped);
+int32_t gpucipher_compute_hash(rc_cipher *c, uintptr_t src, int closer, const uint8_t *nonce, uint8_t *md5);
+int32_t gpucipher_hash_batch(rc_cipher *c, uint64_t n, const uintptr_t *srcs, uint64_t n_nonces, const uint8_t *nonces,
+                             uint8_t *md5, int32_t *errs);
 
 static int failures = 0;
 #define CHECK(c, msg)                          \
@@ -60,9 +64,15 @@ int32_t goRangeSeek(uintptr_t h, int64_t offset, int32_t whence, int64_t limit) 
   return RC_NIL;
 }
 static int64_t open_calls[4][2];
-static int nopen = 0;
+static int nopen = 0, reopen_calls = 0;
 int32_t goOpen(uintptr_t h, int64_t off, int64_t lim, rc_reader *out) {
-  (void)out;
+  if (h == 100) { /* the first open serves a valid header (box 0, no RangeSeeker); the re-open fails */
+    if (reopen_calls++ == 0) {
+      *out = gpucipher_reader(0, 1, 0);
+      return RC_NIL;
+    }
+    return RC_USER_BASE + 42;
+  }
   if (nopen < 4) {
     open_calls[nopen][0] = off;
     open_calls[nopen][1] = lim;
@@ -124,13 +134,45 @@ int main(void) {
   printf("decrypter_errors %d %d %d\n", RC_ERR_BAD_MAGIC, RC_ERR_FILE_TOO_SHORT, RC_USER_BASE + 7);
 
   /* DecryptDataSeek: the opener's error passes through; open arguments as cipher.go:821-859 */
-  d = gpucipher_decrypt_seek(c, 4, 0, -1, &err);
-  CHECK(!d && err == RC_USER_BASE + 4, "open error (offset 0)");
-  d = gpucipher_decrypt_seek(c, 5, 100, 50, &err);
+  int32_t wrapped = -1;
+  d = gpucipher_decrypt_seek(c, 4, 0, -1, &err, &wrapped);
+  CHECK(!d && err == RC_USER_BASE + 4 && wrapped == RC_NIL, "open error (offset 0)");
+  d = gpucipher_decrypt_seek(c, 5, 100, 50, &err, &wrapped);
   CHECK(!d && err == RC_USER_BASE + 5, "open error (offset 100)");
   CHECK(nopen == 2 && open_calls[0][0] == 0 && open_calls[0][1] == -1 && open_calls[1][0] == 0 &&
             open_calls[1][1] == 32,
         "open arguments");
+
+  /* the re-open at the seek offset fails: RC_ERR_REOPEN with the opener's own error behind it
+   * (cipher.go:1011 wraps it with %w), the header reader closed once */
+  static const uint8_t hdr32[32] = "RCLONE\0\0abcdefghijklmnopqrstuvwx";
+  boxes[0] = (box){hdr32, 32, 0, RC_EOF, 0, 0};
+  d = gpucipher_decrypt_seek(c, 100, 70000, -1, &err, &wrapped);
+  CHECK(!d && err == RC_ERR_REOPEN && wrapped == RC_USER_BASE + 42 && reopen_calls == 2 && boxes[0].closes == 1,
+        "re-open error wrapped");
+  printf("reopen_wrapped %d %d\n", err, wrapped);
+
+  /* computeHashWithNonce through the shim: a source failing before its first block returns its
+   * error and is closed once; a nonce count that differs from the source count is refused before
+   * any source is read.  No GPU work is needed for either. */
+  static const uint8_t nonce24[24] = {9};
+  uint8_t md5[16 * 3];
+  boxes[1] = (box){NULL, 0, 0, RC_USER_BASE + 11, 0, 0};
+  CHECK(gpucipher_compute_hash(c, 1, 1, nonce24, md5) == RC_USER_BASE + 11 && boxes[1].closes == 1,
+        "compute hash: reader error, source closed");
+  uintptr_t srcs[3] = {1, 2, 3};
+  int32_t errs[3] = {0, 0, 0};
+  uint8_t nonces[24 * 3] = {0};
+  boxes[1] = (box){NULL, 0, 0, RC_USER_BASE + 11, 0, 0};
+  boxes[2] = (box){NULL, 0, 0, RC_USER_BASE + 12, 0, 0};
+  boxes[3] = (box){NULL, 0, 0, RC_UNEXPECTED_EOF, 0, 0};
+  CHECK(gpucipher_hash_batch(c, 3, srcs, 2, nonces, md5, errs) == RC_ERR_INVALID && boxes[1].reads == 0,
+        "hash batch: nonce count mismatch refused");
+  CHECK(gpucipher_hash_batch(c, 3, srcs, 3, nonces, md5, errs) == RC_NIL && errs[0] == RC_USER_BASE + 11 &&
+            errs[1] == RC_USER_BASE + 12 && errs[2] == RC_UNEXPECTED_EOF && boxes[1].closes == 1 &&
+            boxes[2].closes == 1 && boxes[3].closes == 1,
+        "hash batch: failing sources");
+  printf("hash_batch_errs %d %d %d\n", errs[0], errs[1], errs[2]);
 
   /* encrypter: nonce from the cipher's random source, header served before any block */
   static const uint8_t rnd[24] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};

@@ -17,6 +17,11 @@
 //   * concurrency (meaningful under TSan): many encrypters/decrypters sharing one cipher on
 //     several threads, and one rc_names_run batch over 16 host threads.
 // Exit status 0 and a final "sanitize ok" line mean every check passed.
+#include <sched.h>
+#include <sys/stat.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -29,6 +34,7 @@
 
 #include "../../include/rclone_crypt_gpu.h"
 #include "../../rclone_amd/csrc/xs_host_md5.h"
+#include "../../rclone_amd/csrc/xs_topo.h"
 
 extern "C" {
 void orc_encrypt_file(uint8_t* out, const uint8_t* in, int64_t len, const uint8_t nonce0[24], const uint8_t key[32]);
@@ -666,6 +672,64 @@ static void test_encrypter_md5(rc_cipher* c, const uint8_t key[32]) {
   }
 }
 
+// ---------------------------------------------------------------- node topology (xs_topo.cpp)
+// A fake sysfs tree: the GPU's PCI function on node 1, node 1 = CPU 0 only.  Library threads
+// pinned to node 1 may then run on CPU 0 only; the preferred-node memory policy is scoped.
+static void put_file(const std::string& path, const char* text) {
+  std::string dir;
+  for (size_t i = 1; i < path.size(); i++)
+    if (path[i] == '/') mkdir(path.substr(0, i).c_str(), 0755);
+  FILE* f = fopen(path.c_str(), "w");
+  if (f) {
+    fputs(text, f);
+    fclose(f);
+  }
+}
+static void test_topology() {
+  char tmpl[] = "/tmp/rc_sysfs_XXXXXX";
+  const char* root = mkdtemp(tmpl);
+  CHECK(root != nullptr, "mkdtemp");
+  if (!root) return;
+  const std::string r(root);
+  put_file(r + "/bus/pci/devices/0000:c1:00.0/numa_node", "1\n");
+  put_file(r + "/bus/pci/devices/0000:05:00.0/numa_node", "-1\n");
+  put_file(r + "/devices/system/node/node1/cpulist", "0\n");
+  put_file(r + "/devices/system/node/node2/cpulist", "4-7,12,14-15\n");
+  setenv("RCLONE_AMD_SYSFS_ROOT", root, 1);
+  CHECK(xs::pci_numa_node("0000:C1:00.0") == 1, "bus id -> node (upper-case id)");
+  CHECK(xs::pci_numa_node("0000:05:00.0") == -1 && xs::pci_numa_node("0000:99:00.0") == -1, "unknown node");
+  std::vector<int> cpus;
+  CHECK(xs::node_cpus(2, &cpus) && cpus == std::vector<int>({4, 5, 6, 7, 12, 14, 15}), "cpulist ranges");
+  CHECK(!xs::node_cpus(3, &cpus) && !xs::node_cpus(-1, &cpus), "missing node");
+  CHECK(!xs::parse_cpulist("3-1", &cpus) && !xs::parse_cpulist("x", &cpus), "malformed cpulist");
+  std::vector<int> devs;
+  CHECK(xs::parse_device_list("0,1,1,2", &devs) == 4 && devs == std::vector<int>({0, 1, 1, 2}), "device list repeats");
+  CHECK(xs::parse_device_list(" 3, 4", &devs) == 2 && devs == std::vector<int>({3, 4}), "device list spaces");
+  CHECK(xs::parse_device_list("0,x", &devs) == 1 && xs::parse_device_list("", &devs) == 0, "device list garbage");
+  int on_cpu0 = 0;
+  std::thread t([&] {
+    xs::pin_thread_to_node(1);
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0) on_cpu0 = CPU_COUNT(&set) == 1 && CPU_ISSET(0, &set);
+  });
+  t.join();
+  CHECK(on_cpu0, "thread pinned to the node's CPUs");
+  int mode_before = -1, mode_in = -1, mode_after = -1;
+  unsigned long mask[16] = {0};
+  syscall(SYS_get_mempolicy, &mode_before, mask, 1024ul, nullptr, 0ul);
+  {
+    xs::ScopedMemPolicy pol(0);  // node 0 exists on any Linux machine
+    memset(mask, 0, sizeof mask);
+    syscall(SYS_get_mempolicy, &mode_in, mask, 1024ul, nullptr, 0ul);
+    CHECK(mode_in == 1 && (mask[0] & 1ul), "preferred node 0 inside the scope (mode %d)", mode_in);
+  }
+  syscall(SYS_get_mempolicy, &mode_after, mask, 1024ul, nullptr, 0ul);
+  CHECK(mode_after == mode_before, "policy restored (%d vs %d)", mode_after, mode_before);
+  unsetenv("RCLONE_AMD_SYSFS_ROOT");
+  (void)!system(("rm -rf " + r).c_str());
+}
+
 // ---------------------------------------------------------------- concurrency (TSan)
 static void test_concurrency(rc_cipher* c, const uint8_t key[32]) {
   std::atomic<int> bad{0};
@@ -763,6 +827,7 @@ int main(int argc, char** argv) {
     test_damaged(c, key);
     test_reader_errors(c, key);
     test_hash_with_nonce(c, key);
+    test_topology();
     test_encrypter_md5(c, key);
     test_seek_grid(c, key);
     test_names(c);

@@ -54,6 +54,8 @@ struct xs_pool {
 extern "C" {
 const char* xs_last_error(void) { return xs::g_err.c_str(); }
 void* xs_host_alloc(size_t bytes) { return malloc(bytes ? bytes : 1); }
+void* xs_host_alloc_node(size_t bytes, int) { return malloc(bytes ? bytes : 1); }
+int xs_engine_numa_node(const xs_engine*) { return -1; }
 void xs_host_free(void* p) { free(p); }
 
 xs_pool* xs_pool_create(const int*, int, uint32_t, int) { return new xs_pool(); }

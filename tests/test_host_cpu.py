@@ -113,3 +113,28 @@ def test_device_entry_points_reject_bad_arguments():
     assert lib.xs_verify_blocks_dev(aligned + 4, 1, 0, 1, 7, ctypes.byref(word), None) == XS_ERR_INVALID
     assert lib.xs_verify_blocks_dev(aligned, 1, 0, 0, 7, ctypes.byref(word), None) == XS_ERR_INVALID
     assert lib.xs_fill_blocks_dev(aligned, 1, 0, 0, 7, None) == XS_ERR_INVALID
+
+
+def test_reopen_error_keeps_the_openers_error():
+    # DecryptDataSeek at an offset: the header opens, the re-open at the block fails; the error is
+    # "couldn't reopen file with offset and limit: %w" around the opener's own error
+    # (cipher.go:1011) -- host-only, no GPU involved (rc_decrypt_data_seek_ex)
+    from tests.go_readers import Buffer
+
+    class Gone(Exception):
+        pass
+
+    c = crypt.Cipher("potato", "")
+    calls = []
+
+    def open_fn(off, lim):
+        calls.append((off, lim))
+        if len(calls) == 1:
+            return Buffer(b"RCLONE\x00\x00" + bytes(range(24)))
+        raise Gone("object not found")
+
+    with pytest.raises(crypt.CryptError) as ei:
+        c.decrypt_data_seek(open_fn, 70000, -1)
+    assert "couldn't reopen file with offset and limit: object not found" in str(ei.value)
+    assert isinstance(ei.value.__cause__, Gone)
+    assert calls == [(0, 32), (32 + 65552, -1)]
