@@ -160,17 +160,25 @@ class ClockProbe:
                                        "stream over the first 80% of the timed steps"}
 
 
-def issue_bound(valu_insts, ms, clock_hz=None):
-    """VALU roofline of a launch: integer VALU wave-instructions (rocprofv3 SQ_INSTS_VALU) issued
-    per second against the chip's issue peak, 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64
-    integer instruction (measured on gfx950: tools/microbench/issuebench.hip) = 614.4 G
-    wave-instructions/s; and the same bound at the clock measured in the timed window."""
+def issue_bound(valu_insts, ms, clock_hz=None, mfma_insts=None):
+    """VALU roofline of a launch: integer VALU wave-instructions issued per second against the
+    chip's issue peak, 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 integer instruction
+    (measured on gfx950: tools/microbench/issuebench.hip) = 614.4 G wave-instructions/s; and the
+    same bound at the clock measured in the timed window.  rocprofv3's SQ_INSTS_VALU also counts
+    the matrix-core Poly1305's v_mfma_i32_16x16x64_i8 (SQ_INSTS_VALU_MFMA_I8), which execute on
+    the SIMD's matrix pipe: the bound counts the other VALU instructions (valu_insts - mfma_insts)
+    and reports the MFMAs beside it.  Without an MFMA count (older PMC stamps) every instruction
+    is counted."""
     if not valu_insts:
         return None
+    vector = valu_insts - (mfma_insts or 0)
     peak = SIMDS * CLOCK_HZ / VALU_CYC / 1e9
-    achieved = valu_insts / (ms * 1e-3) / 1e9
+    achieved = vector / (ms * 1e-3) / 1e9
     res = {"bound": "valu", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "G wave-instr/s",
            "frac": round(achieved / peak, 4), "valu_wave_insts": valu_insts, "cycles_per_inst": VALU_CYC}
+    if mfma_insts is not None:
+        res.update({"mfma_wave_insts": mfma_insts, "vector_wave_insts": vector,
+                    "counted": "SQ_INSTS_VALU - SQ_INSTS_VALU_MFMA_I8 (MFMAs run on the matrix pipe)"})
     if clock_hz:
         peak_w = SIMDS * clock_hz / VALU_CYC / 1e9
         res.update({"window_clock_ghz": round(clock_hz / 1e9, 4), "peak_at_window_clock": round(peak_w, 1),
@@ -699,11 +707,13 @@ def main():
                          "alg_bytes_per_launch": ALG_BYTES_SEAL * nb,
                          "traffic_source": tr.get("source") if tr else stale,
                          "traffic_git_head": tr.get("git_head"),
-                         "valu": issue_bound(per("seal_valu_wave_insts_per_launch"), seal_avg, clk_hz),
+                         "valu": issue_bound(per("seal_valu_wave_insts_per_launch"), seal_avg, clk_hz,
+                                             per("seal_mfma_wave_insts_per_launch")),
                          "open": {"kernel": "xs_open", "achieved": round(ach_open, 1),
                                   "frac": round(ach_open / HBM_PEAK_GBS, 4), "kernel_ms_avg": round(open_avg, 4),
                                   "traffic": per("open_bytes_per_launch"),
-                                  "valu": issue_bound(per("open_valu_wave_insts_per_launch"), open_avg, clk_hz)}},
+                                  "valu": issue_bound(per("open_valu_wave_insts_per_launch"), open_avg, clk_hz,
+                                                      per("open_mfma_wave_insts_per_launch"))}},
             "clock": clock,
             "warmup_s": round(warm_s, 3), "warmup_steps": nwarm,
             "counters": {"blocks": int(counters[0].item()), "bytes": total_bytes,

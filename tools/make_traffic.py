@@ -5,7 +5,8 @@ xs_crypt launch: profiles/pmc_traffic.json (read by bench.py as roofline.traffic
 Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE counts exactly half the
 bytes of a wide (16 B/lane) streaming read -- global_load and LDS-DMA alike -- so reads =
 2 x FETCH_SIZE; WRITE_SIZE is exact for 16 B/lane stores.  Both are in KiB.
-Also records SQ_INSTS_VALU (wave-instructions) per launch for the VALU issue bound."""
+Also records SQ_INSTS_VALU (wave-instructions) and SQ_INSTS_VALU_MFMA_I8 per launch for the VALU
+issue bound (MFMAs run on the matrix pipe: the bound counts SQ_INSTS_VALU - SQ_INSTS_VALU_MFMA_I8)."""
 import json
 import os
 import subprocess
@@ -30,7 +31,7 @@ def git_head(root=ROOT):
 def main():
     d, out = sys.argv[1], sys.argv[2]
     acc = load(d)
-    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU ({d}), one pass per counter group, "
+    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU / SQ_INSTS_VALU_MFMA_I8 ({d}), one pass per counter group, "
                      "reads x2 (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md HBM section)",
            "blocks_per_launch": int(sys.argv[3]) if len(sys.argv) > 3 else 100_000,
            "kernel_sources_sha256": kernel_sources_sha256(),
@@ -48,6 +49,12 @@ def main():
                 res[f"{key}_valu_wave_insts_per_launch"] = round(sum(cs["SQ_INSTS_VALU"]) / len(cs["SQ_INSTS_VALU"]))
                 if "SQ_WAVES" in cs:
                     res[f"{key}_waves_per_launch"] = round(sum(cs["SQ_WAVES"]) / len(cs["SQ_WAVES"]))
+            # the matrix-core Poly1305 (v_mfma_i32_16x16x64_i8): SQ_INSTS_VALU counts these too, but
+            # they execute on the SIMD's matrix pipe, so the VALU issue bound uses the difference
+            for cname, rkey in (("SQ_INSTS_VALU_MFMA_I8", "mfma_wave_insts"), ("SQ_VALU_MFMA_BUSY_CYCLES", "mfma_busy_cycles"),
+                                ("SQ_VALU_MFMA_COEXEC_CYCLES", "mfma_coexec_cycles"), ("GRBM_GUI_ACTIVE", "gui_active_cycles")):
+                if name in k and cname in cs:
+                    res[f"{key}_{rkey}_per_launch"] = round(sum(cs[cname]) / len(cs[cname]))
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
