@@ -55,11 +55,18 @@ class HostMd5 {
       uint32_t m[16];
       memcpy(m, p, 64);  // little-endian host
       uint32_t a = a0, b = b0, c = c0, d = d0;
-#define XS_F(x, y, z) ((z) ^ ((x) & ((y) ^ (z))))
-#define XS_G(x, y, z) ((y) ^ ((z) & ((x) ^ (y))))
-#define XS_H(x, y, z) ((x) ^ (y) ^ (z))
-#define XS_I(x, y, z) ((y) ^ ((x) | ~(z)))
-#define XS_STEP(f, w, x, y, z, k, t, s) w = x + rol(w + f(x, y, z) + m[k] + (t), s)
+// The step is w = x + rol(w + f(x, y, z) + m + t, s) with x the newest word.  Everything that
+// does not depend on x is added first, so the chain through x is as short as the function allows
+// (one step's latency is the stream's rate: MD5 is one dependency chain):
+//   F = z ^ (x & (y ^ z)): and, xor;  G = (x & z) + (y & ~z) (disjoint bits): the y & ~z half
+//   joins the early sum, leaving one and;  H = x ^ (y ^ z): one xor;  I = y ^ (x | ~z): or, xor.
+#define XS_F(w, x, y, z, mk) w += (mk); w += (z) ^ ((x) & ((y) ^ (z)))
+#define XS_G(w, x, y, z, mk) w += (mk) + ((y) & ~(z)); w += (x) & (z)
+#define XS_H(w, x, y, z, mk) w += (mk); w += (x) ^ ((y) ^ (z))
+#define XS_I(w, x, y, z, mk) w += (mk); w += (y) ^ ((x) | ~(z))
+#define XS_STEP(f, w, x, y, z, k, t, s) \
+  f(w, x, y, z, m[k] + (uint32_t)(t));   \
+  w = x + rol(w, s)
       XS_STEP(XS_F, a, b, c, d, 0, 0xd76aa478, 7);
       XS_STEP(XS_F, d, a, b, c, 1, 0xe8c7b756, 12);
       XS_STEP(XS_F, c, d, a, b, 2, 0x242070db, 17);

@@ -60,67 +60,13 @@
 #include <vector>
 
 #include "../include/rclone_crypt_gpu.h"
+#include "../rclone_amd/csrc/xs_host_md5.h"
 
 // ---------------------------------------------------------------- MD5 (RFC 1321), host
-struct Md5 {
-  uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
-  uint8_t buf[64];
-  uint64_t n = 0;
-  static uint32_t rol(uint32_t x, int c) { return (x << c) | (x >> (32 - c)); }
-  void block(const uint8_t* p) {
-    static const uint32_t K[64] = {
-        0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
-        0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
-        0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
-        0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
-        0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
-        0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
-        0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
-        0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
-    static const int R[16] = {7, 12, 17, 22, 5, 9, 14, 20, 4, 11, 16, 23, 6, 10, 15, 21};
-    uint32_t m[16];
-    memcpy(m, p, 64);  // little-endian host
-    uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
-    for (int i = 0; i < 64; i++) {
-      uint32_t f;
-      int g;
-      if (i < 16) { f = (b & c) | (~b & d); g = i; }
-      else if (i < 32) { f = (d & b) | (~d & c); g = (5 * i + 1) & 15; }
-      else if (i < 48) { f = b ^ c ^ d; g = (3 * i + 5) & 15; }
-      else { f = c ^ (b | ~d); g = (7 * i) & 15; }
-      const uint32_t t = d;
-      d = c;
-      c = b;
-      b = b + rol(a + f + K[i] + m[g], R[(i >> 4) * 4 + (i & 3)]);
-      a = t;
-    }
-    h[0] += a; h[1] += b; h[2] += c; h[3] += d;
-  }
-  void update(const uint8_t* p, size_t len) {
-    size_t have = n & 63;
-    n += len;
-    if (have) {
-      const size_t k = std::min(len, 64 - have);
-      memcpy(buf + have, p, k);
-      p += k;
-      len -= k;
-      if (have + k < 64) return;
-      block(buf);
-    }
-    for (; len >= 64; p += 64, len -= 64) block(p);
-    memcpy(buf, p, len);
-  }
-  void final(uint8_t out[16]) {
-    const uint64_t bits = n * 8;
-    const uint8_t one = 0x80, zero = 0;
-    update(&one, 1);
-    while ((n & 63) != 56) update(&zero, 1);
-    uint8_t lb[8];
-    for (int i = 0; i < 8; i++) lb[i] = (uint8_t)(bits >> (8 * i));
-    update(lb, 8);
-    memcpy(out, h, 16);
-  }
-};
+// The memory remote's Object.Hash and the reading thread's TeeReader (--tee reader) hash with the
+// same host MD5 the library uses (about the speed of Go's crypto/md5 assembly / OpenSSL), so the
+// tee placements compare like for like.
+using Md5 = xs::HostMd5;
 
 // ---------------------------------------------------------------- SHA-256 (FIPS 180-4), host
 // for --anchor: digests of sampled stored crypt files, checked by the test suite against the
