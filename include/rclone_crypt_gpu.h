@@ -355,8 +355,9 @@ int32_t rc_hash_batch_with_nonce(rc_cipher *c, uint64_t n, const rc_reader *srcs
  * group-committed into shared launches), MD5s "RCLONE\0\0" || nonce || wire blocks on host cores
  * (one core hashes a stream ~10x faster than one GPU lane), overlapping batch k's hash with batch
  * k+1's read and seal, then closes src if it has a close function (defer fs.CheckClose(in, &err)).
- * Returns RC_NIL with md5 set, the reader's non-EOF error or the closer's error (the reference wraps
- * them as "failed to hash data: %w"), or RC_ERR_GPU. */
+ * Returns RC_NIL with md5 set; the reader's non-EOF error (io.Copy's, which the reference wraps as
+ * "failed to hash data: %w"); the closer's error when every read succeeded -- md5 is then set too,
+ * as the reference returns hashStr alongside CheckClose's error; or RC_ERR_GPU. */
 int32_t rc_compute_hash_with_nonce(rc_cipher *c, rc_reader src, const uint8_t nonce[24], uint8_t md5[16]);
 
 /* ------------------------------------------------------------------------------------

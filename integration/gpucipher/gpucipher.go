@@ -31,6 +31,7 @@ import "C"
 
 import (
 	"context"
+	"encoding/hex"
 	"errors"
 	"fmt"
 	"io"
@@ -127,9 +128,10 @@ func (t *errTable) err(code C.int32_t) error {
 // ---------------------------------------------------------------------------- callbacks
 
 type readerBox struct {
-	r io.Reader
-	t *errTable
-	s *openState // the decrypter's state (its RangeSeek context), nil for an encrypter's source
+	r       io.Reader
+	t       *errTable
+	s       *openState // the decrypter's state (its RangeSeek context), nil for an encrypter's source
+	readErr bool       // a Read returned an error other than io.EOF
 }
 
 //export goRead
@@ -137,6 +139,9 @@ func goRead(h C.uintptr_t, p *C.uint8_t, n C.int64_t, errp *C.int32_t) C.int64_t
 	b := cgo.Handle(h).Value().(*readerBox)
 	buf := unsafe.Slice((*byte)(unsafe.Pointer(p)), int(n)) // library-owned pinned staging
 	got, err := b.r.Read(buf)
+	if err != nil && err != io.EOF {
+		b.readErr = true
+	}
 	*errp = b.t.code(err)
 	return C.int64_t(got)
 }
@@ -264,33 +269,37 @@ func New(dataKey, nameKey *[32]byte, nameTweak *[16]byte, passBadBlocks bool) (*
 	return c, nil
 }
 
-// ComputeHashWithNonce is computeHashWithNonce (crypt.go:784-806) for MD5: src (already opened,
-// as crypt.go opens it) is read to EOF, sealed with nonce on the GPU -- concurrent checkers'
-// seals share launches -- and "RCLONE\0\0" || nonce || wire blocks is MD5'd on host cores; src is
-// closed when it is an io.Closer (defer fs.CheckClose(in, &err)).  The only change crypt.go needs:
+// ComputeHashWithNonce is computeHashWithNonce (crypt.go:784-806) for MD5 after src.Open: in is
+// read to EOF, sealed with nonce on the GPU -- concurrent checkers' seals share launches -- and
+// "RCLONE\0\0" || nonce || wire blocks is MD5'd on host cores; in is closed when it is an
+// io.Closer (the library does what `defer fs.CheckClose(in, &err)` does).  It returns what the
+// reference returns from that point: ("", "failed to hash data: %w") for a read error, the hex
+// digest and nil, or the hex digest with the close error.  crypt.go's change, after src.Open:
 //
 //	if f.cipher.gpu != nil && hashType == hash.MD5 {
-//		sum, err := f.cipher.gpu.ComputeHashWithNonce((*[24]byte)(&nonce), in)
-//		if err != nil {
-//			return "", fmt.Errorf("failed to hash data: %w", err)
-//		}
-//		return hex.EncodeToString(sum[:]), nil
+//		return f.cipher.gpu.ComputeHashWithNonce((*[24]byte)(&nonce), in)
 //	}
-func (c *Cipher) ComputeHashWithNonce(nonce *[24]byte, src io.Reader) (sum [16]byte, err error) {
+//	defer fs.CheckClose(in, &err) // the Go path, unchanged
+func (c *Cipher) ComputeHashWithNonce(nonce *[24]byte, in io.Reader) (hashStr string, err error) {
+	var sum [16]byte
 	t := &errTable{}
-	hd := cgo.NewHandle(&readerBox{r: src, t: t})
+	box := &readerBox{r: in, t: t}
+	hd := cgo.NewHandle(box)
 	defer hd.Delete()
-	_, closer := src.(io.Closer)
+	_, closer := in.(io.Closer)
 	rc := C.gpucipher_compute_hash(c.h, C.uintptr_t(hd), cbool(closer), (*C.uint8_t)(unsafe.Pointer(&nonce[0])),
 		(*C.uint8_t)(unsafe.Pointer(&sum[0])))
 	runtime.KeepAlive(c)
-	if rc != C.RC_NIL {
-		if rc == C.RC_ERR_GPU {
-			return sum, fmt.Errorf("gpucipher: %s", C.GoString(C.xs_last_error()))
-		}
-		return sum, t.err(rc)
+	switch {
+	case rc == C.RC_NIL:
+		return hex.EncodeToString(sum[:]), nil
+	case rc == C.RC_ERR_GPU:
+		return "", fmt.Errorf("failed to hash data: gpucipher: %s", C.GoString(C.xs_last_error()))
+	case box.readErr || !closer:
+		return "", fmt.Errorf("failed to hash data: %w", t.err(rc)) // io.Copy's error
+	default:
+		return hex.EncodeToString(sum[:]), t.err(rc) // every read succeeded: CheckClose's error
 	}
-	return sum, nil
 }
 
 // ---------------------------------------------------------------------------- encrypter

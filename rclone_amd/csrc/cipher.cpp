@@ -1015,10 +1015,12 @@ extern "C" int32_t rc_compute_hash_with_nonce(rc_cipher* c, rc_reader src, const
     }
   }
   w.wait(&job);
+  // the reference returns hashStr with CheckClose's error: the digest is set whenever the reads
+  // succeeded, also when the close then fails
+  if (err == RC_NIL) m.final(md5);
   if (src.close) {  // defer fs.CheckClose(in, &err)
     const int32_t ce = src.close(src.user);
     if (err == RC_NIL && ce != RC_NIL) err = ce;
   }
-  if (err == RC_NIL) m.final(md5);
   return err;
 }

@@ -615,12 +615,14 @@ static void test_hash_with_nonce(rc_cipher* c, const uint8_t key[32]) {
     const int32_t err2 = rc_compute_hash_with_nonce(c, rc_reader{src_read, src_close_fail, nullptr, &t}, nonce.data(), got);
     CHECK(err2 == t.fail_err && t.closes == 1, "hash reader+close error at %ld: %d", (long)q, err2);
   }
-  Src s;  // clean read, failing close: the close error
+  Src s;  // clean read, failing close: the close error, with the digest (hashStr, CheckClose's err)
   s.p = plain.data();
   s.n = plain.size();
   uint8_t got[16];
   const int32_t err = rc_compute_hash_with_nonce(c, rc_reader{src_read, src_close_fail, nullptr, &s}, nonce.data(), got);
-  CHECK(err == RC_USER_BASE + 9 && s.closes == 1, "hash close error: %d", err);
+  const std::vector<uint8_t> pf = oracle_file(plain, nonce.data(), key);
+  CHECK(err == RC_USER_BASE + 9 && s.closes == 1 && std::vector<uint8_t>(got, got + 16) == md5_of(pf.data(), pf.size()),
+        "hash close error: %d", err);
   Src n;  // no close function (io.NopCloser)
   n.p = plain.data();
   n.n = 100;
