@@ -226,6 +226,7 @@ class Cipher(NameCipherMixin):
     def __init__(self, password: str = "", salt: str = "", pass_bad_blocks: bool = False, batch_blocks: int = 64,
                  mode: int = NAME_ENCRYPTION_STANDARD, dir_name_encrypt: bool = True, enc=None):
         e = ctypes.c_int32(0)
+        self._free = _lib.lib().rc_cipher_free
         self._h = _lib.lib().rc_cipher_new(password.encode(), salt.encode(), ctypes.byref(e))
         _raise(e.value)
         self.set_name_encryption(mode, dir_name_encrypt, enc)
@@ -235,9 +236,10 @@ class Cipher(NameCipherMixin):
         self.batch_blocks = batch_blocks
 
     def __del__(self):
-        h = getattr(self, "_h", None)
-        if h:
-            _lib.lib().rc_cipher_free(h)
+        # at interpreter exit the module globals may already be gone: bound function only
+        h, free = getattr(self, "_h", None), getattr(self, "_free", None)
+        if h and free is not None:
+            free(h)
             self._h = None
 
     def key(self, password: str, salt: str = ""):
@@ -429,15 +431,17 @@ class Encrypter:
         nb = bytes(nonce) if nonce is not None else None
         if nb is not None and len(nb) != 24:
             raise ValueError("nonce must be 24 bytes")
+        self._free = _lib.lib().rc_encrypter_free
         self._h = _lib.lib().rc_encrypt_data(cipher._h, self._bridge.c, nb, ctypes.byref(e))
         if not self._h:
             _raise(e.value, wrapped=RC_EOF)
             raise GPUError(GPUError.message)
 
     def __del__(self):
-        h = getattr(self, "_h", None)
-        if h:
-            _lib.lib().rc_encrypter_free(h)
+        # at interpreter exit the module globals may already be gone: bound function only
+        h, free = getattr(self, "_h", None), getattr(self, "_free", None)
+        if h and free is not None:
+            free(h)
             self._h = None
 
     @property
@@ -490,6 +494,7 @@ class Decrypter:
     def __init__(self, cipher: Cipher, reader, open_fn=None, offset=0, limit=-1):
         self._cipher = cipher
         self._bridges = []
+        self._free = _lib.lib().rc_decrypter_free
         e = ctypes.c_int32(0)
         if open_fn is None:
             b = _ReaderBridge(reader)
@@ -516,9 +521,10 @@ class Decrypter:
             raise GPUError(GPUError.message)
 
     def __del__(self):
-        h = getattr(self, "_h", None)
-        if h:
-            _lib.lib().rc_decrypter_free(h)
+        # at interpreter exit the module globals may already be gone: bound function only
+        h, free = getattr(self, "_h", None), getattr(self, "_free", None)
+        if h and free is not None:
+            free(h)
             self._h = None
 
     @property
