@@ -36,6 +36,7 @@ BLOCK_SIZE = 65552
 ALG_BYTES_SEAL = 65536 + 65552
 ALG_BYTES_OPEN = 65552 + 65536 + 1
 VALU_CYC, SIMDS, CLOCK_HZ = 4, 256 * 4, 2.4e9
+MFMA_HOLD_CYC = 8  # v_mfma_i32_16x16x64_i8: 16 cycles on the matrix pipe, vector issue held for 8
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -179,6 +180,11 @@ def issue_bound(valu_insts, ms, clock_hz=None, mfma_insts=None):
     if mfma_insts is not None:
         res.update({"mfma_wave_insts": mfma_insts, "vector_wave_insts": vector,
                     "counted": "SQ_INSTS_VALU - SQ_INSTS_VALU_MFMA_I8 (MFMAs run on the matrix pipe)"})
+        if clock_hz:
+            # upper model: each MFMA also holds the SIMD's vector issue for 8 of its 16 cycles
+            # (MI355X_MICROARCH.md constants, 'vector-instruction ISSUE cost')
+            cyc = (vector * VALU_CYC + mfma_insts * MFMA_HOLD_CYC) / SIMDS
+            res["frac_at_window_clock_with_mfma_hold"] = round(cyc / (ms * 1e-3 * clock_hz), 4)
     if clock_hz:
         peak_w = SIMDS * clock_hz / VALU_CYC / 1e9
         res.update({"window_clock_ghz": round(clock_hz / 1e9, 4), "peak_at_window_clock": round(peak_w, 1),
