@@ -35,22 +35,27 @@ class Md5Workers {
   Md5Workers(int max_threads, int node) : max_(max_threads), node_(node) {}
   int max_threads() const { return max_; }
   // j->st is updated with j->p[0:n] on a worker; the caller waits with wait() before touching
-  // j->st or reusing j->p.  With no workers (max_threads 0) the hash runs here.
+  // j->st or reusing j->p.  When every worker is taken (or there are none: max_threads 0) the
+  // hash runs here, on the caller's thread: a queued job would only wait for a worker, while the
+  // caller can hash it now -- so with more streams than workers each stream still has a core.
   void submit(Md5Job* j) {
-    if (max_ <= 0) {
-      j->st->update(j->p, j->n);
-      return;
+    if (max_ > 0) {
+      std::unique_lock<std::mutex> g(mu_);
+      const bool spawn = (int)q_.size() >= idle_ && (int)th_.size() < max_;
+      if ((int)q_.size() < idle_ || spawn) {
+        j->owner = this;
+        j->busy.store(1, std::memory_order_relaxed);
+        q_.push_back(j);
+        if (spawn)
+          th_.emplace_back([this] {
+            pin_thread_to_node(node_);  // the node of the engines whose streams it hashes
+            run();
+          });
+        cv_.notify_one();
+        return;
+      }
     }
-    j->owner = this;
-    j->busy.store(1, std::memory_order_relaxed);
-    std::lock_guard<std::mutex> g(mu_);
-    q_.push_back(j);
-    if ((int)th_.size() < max_ && idle_ == 0)
-      th_.emplace_back([this] {
-        pin_thread_to_node(node_);  // the node of the engines whose streams it hashes
-        run();
-      });
-    cv_.notify_one();
+    j->st->update(j->p, j->n);
   }
   void wait(Md5Job* j) const {
     if (!j->busy.load(std::memory_order_acquire)) return;
