@@ -19,7 +19,9 @@
 // at which each error surfaces and the nonce after EOF are those of the reference.
 #include <sys/random.h>
 
+#include <atomic>
 #include <cerrno>
+#include <cstdio>
 #include <cstdlib>
 #include <algorithm>
 #include <chrono>
@@ -349,6 +351,49 @@ extern "C" const char* rc_error_string(int32_t e) {
   }
 }
 
+// ---------------------------------------------------------------- phase times (diagnostic)
+// RCLONE_AMD_PHASES=1: where the streaming refills and per-object hashes spend their time,
+// summed over threads and printed to stderr at exit (source reads, GPU seals, MD5 waits / inline
+// MD5, consumer-side copies are the rest).  Off: one predictable branch per refill.
+namespace {
+enum Phase { kEncRead, kEncSeal, kEncWait, kEncInline, kEncRefills, kHashRead, kHashSeal, kHashWait, kHashInline,
+             kHashCalls, kNPhase };
+std::atomic<uint64_t> g_phase[kNPhase];
+bool phases_on() {
+  static const bool on = [] {
+    const char* v = getenv("RCLONE_AMD_PHASES");
+    if (!v || atoi(v) == 0) return false;
+    atexit([] {
+      static const char* names[kNPhase] = {"enc_read", "enc_seal", "enc_md5_wait", "enc_md5_inline", "enc_refills",
+                                           "hash_read", "hash_seal", "hash_md5_wait", "hash_md5_inline", "hash_calls"};
+      fprintf(stderr, "{\"rclone_amd_phases\": {");
+      for (int i = 0; i < kNPhase; i++) {
+        const bool count = i == kEncRefills || i == kHashCalls;
+        fprintf(stderr, "%s\"%s%s\": %.4f", i ? ", " : "", names[i], count ? "" : "_s",
+                count ? (double)g_phase[i].load() : g_phase[i].load() * 1e-9);
+      }
+      fprintf(stderr, "}}\n");
+    });
+    return true;
+  }();
+  return on;
+}
+struct PhaseClock {  // adds the time since the last mark to a phase
+  bool on = phases_on();
+  std::chrono::steady_clock::time_point t = on ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
+  void mark(Phase p) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    g_phase[p].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(n - t).count(),
+                         std::memory_order_relaxed);
+    t = n;
+  }
+  void count(Phase p) {
+    if (on) g_phase[p].fetch_add(1, std::memory_order_relaxed);
+  }
+};
+}  // namespace
+
 // ---------------------------------------------------------------- encrypter
 // Read-ahead: the first refill of a stream (and the first after a seek) reads exactly one block,
 // as encrypter.Read / fillBuffer do (cipher.go:726-741, :862-898), so a slow or streaming source
@@ -473,6 +518,8 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
         (fh->md5_on && !fh->wire2.ensure((size_t)fh->c->batch_blocks * kBlockSize, node)))
       return enc_finish(fh, RC_ERR_GPU, err);
     const auto t0 = std::chrono::steady_clock::now();
+    PhaseClock pc;
+    pc.count(kEncRefills);
     int64_t total = 0;
     uint32_t nb = 0;
     int32_t first_err = RC_NIL;
@@ -494,14 +541,17 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
     // with the tee hash on, seal into the wire buffer that is neither served nor being hashed
     const bool into2 = fh->md5_on && !fh->wsel;
     uint8_t* out = into2 ? fh->wire2.p : fh->wire.p;
+    pc.mark(kEncRead);
     if (xs_engine_seal(fh->eng, fh->c->data_key, fh->nonce, 0, fh->plain.p, (uint64_t)total, out) != XS_OK)
       return enc_finish(fh, RC_ERR_GPU, err);
+    pc.mark(kEncSeal);
     fh->buf_index = 0;
     fh->buf_size = total + (int64_t)nb * kBlockHdr;
     rc_nonce_add(fh->nonce, nb);  // nonce.increment() once per sealed block
     if (fh->md5_on) {
       auto& w = xs::md5_workers(node);
       w.wait(&fh->job);  // the previous batch is hashed: md5 covers everything served so far
+      pc.mark(kEncWait);
       fh->md5_cur = fh->md5;
       fh->wsel = into2;
       fh->job.st = &fh->md5;
@@ -509,6 +559,7 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
       fh->job.n = (size_t)fh->buf_size;
       if (fh->buf_size < kInlineMd5) fh->md5.update(out, (size_t)fh->buf_size);
       else w.submit(&fh->job);
+      pc.mark(kEncInline);
     }
   }
   int64_t m = fh->buf_size - fh->buf_index;
@@ -974,6 +1025,8 @@ extern "C" int32_t rc_compute_hash_with_nonce(rc_cipher* c, rc_reader src, const
   xs::Md5Job job;
   job.st = &m;
   int32_t err = RC_NIL;
+  PhaseClock pc;
+  pc.count(kHashCalls);
   for (int k = 0;; k ^= 1) {
     if (!plain.ensure((size_t)batch * kBlockData, node) || !wire[k].ensure((size_t)batch * kBlockSize, node)) {
       err = RC_ERR_GPU;
@@ -996,18 +1049,22 @@ extern "C" int32_t rc_compute_hash_with_nonce(rc_cipher* c, rc_reader src, const
         break;
       }
     }
+    pc.mark(kHashRead);
     if (nb > 0) {
       if (!eng || xs_engine_seal(eng, c->data_key, n, 0, plain.p, (uint64_t)total, wire[k].p) != XS_OK) {
         err = RC_ERR_GPU;
         break;
       }
+      pc.mark(kHashSeal);
       rc_nonce_add(n, nb);
       w.wait(&job);  // batch k-1 hashed (its buffer is the one sealed into next)
+      pc.mark(kHashWait);
       job.p = wire[k].p;
       job.n = (size_t)(total + (int64_t)nb * kBlockHdr);
       // the stream's (probably) last batch is hashed here: nothing is left to overlap it with
       if (end || short_read || (int64_t)job.n < kInlineMd5) m.update(job.p, job.n);
       else w.submit(&job);
+      pc.mark(kHashInline);
     }
     if (end) {
       err = e == RC_EOF ? RC_NIL : e;
