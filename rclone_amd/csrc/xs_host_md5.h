@@ -30,6 +30,30 @@ class HostMd5 {
     }
     memcpy(buf_, p, len);
   }
+  // For an asynchronous block engine (md5_x16.h): the four state words, and the split of an
+  // update into what must run here and the whole blocks the engine may run later.  begin_blocks
+  // hashes the bytes completing a pending partial block, counts every byte and buffers the
+  // trailing partial block; it returns the whole blocks in between (*nblk of them), which must be
+  // applied to state() before the next update or final.
+  uint32_t* state() { return h_; }
+  const uint8_t* begin_blocks(const uint8_t* p, size_t len, size_t* nblk) {
+    size_t have = (size_t)(n_ & 63);
+    n_ += len;
+    if (have) {
+      size_t k = 64 - have < len ? 64 - have : len;
+      memcpy(buf_ + have, p, k);
+      p += k;
+      len -= k;
+      if (have + k == 64) blocks(buf_, 1);
+      else {
+        *nblk = 0;
+        return p;
+      }
+    }
+    *nblk = len / 64;
+    memcpy(buf_, p + (len & ~(size_t)63), len & 63);
+    return p;
+  }
   void final(uint8_t out[16]) {
     const uint64_t bits = n_ * 8;
     uint8_t pad[72] = {0x80};
