@@ -226,6 +226,9 @@ int xs_pci_numa_node(const char *pci_bus_id); /* <root>/bus/pci/devices/<id>/num
 int xs_numa_node_cpus(int node, int *cpus, int cap);
 /* Parse a device list as RCLONE_AMD_DEVICES ("0,1,1,2": repeats allowed); returns the count. */
 int xs_parse_device_list(const char *list, int *out, int cap);
+/* CPUs this process may use: its affinity mask capped by the cgroup CPU quota (cpu.max under the
+ * sysfs root; RCLONE_AMD_CPUS overrides).  The host MD5 tiers size themselves by it. */
+int xs_effective_cpus(void);
 
 /* ------------------------------------------------------------------------------------
  * rc_*: backend/crypt/cipher.go data API.

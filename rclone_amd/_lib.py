@@ -84,6 +84,7 @@ _SIGS = [
     ("xs_pci_numa_node", ctypes.c_int, [ctypes.c_char_p]),
     ("xs_numa_node_cpus", ctypes.c_int, [ctypes.c_int, vp, ctypes.c_int]),
     ("xs_parse_device_list", ctypes.c_int, [ctypes.c_char_p, vp, ctypes.c_int]),
+    ("xs_effective_cpus", ctypes.c_int, []),
     ("xs_host_free", None, [vp]),
     # cipher.go mirror
     ("rc_cipher_new", vp, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(i32)]),

@@ -45,7 +45,7 @@ def needs_build():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = sources() + [os.path.join(CSRC, h) for h in ("xs_internal.h", "xs_aes.h", "rc_internal.h", "xs_host_md5.h", "md5_workers.h", "xs_topo.h")] + [
+    deps = sources() + [os.path.join(CSRC, h) for h in ("xs_internal.h", "xs_aes.h", "rc_internal.h", "xs_host_md5.h", "md5_workers.h", "md5_x16.h", "xs_topo.h")] + [
                         os.path.join(os.path.dirname(HERE), "include", "rclone_crypt_gpu.h")]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 

@@ -372,7 +372,10 @@ bool phases_on() {
         fprintf(stderr, "%s\"%s%s\": %.4f", i ? ", " : "", names[i], count ? "" : "_s",
                 count ? (double)g_phase[i].load() : g_phase[i].load() * 1e-9);
       }
-      fprintf(stderr, "}}\n");
+      auto& t = xs::md5_tier_stats();
+      fprintf(stderr, ", \"md5_jobs_worker\": %llu, \"md5_jobs_inline\": %llu, \"md5_jobs_lanes\": %llu}}\n",
+              (unsigned long long)t.worker.load(), (unsigned long long)t.inline_.load(),
+              (unsigned long long)t.lanes.load());
     });
     return true;
   }();
@@ -1061,9 +1064,10 @@ extern "C" int32_t rc_compute_hash_with_nonce(rc_cipher* c, rc_reader src, const
       pc.mark(kHashWait);
       job.p = wire[k].p;
       job.n = (size_t)(total + (int64_t)nb * kBlockHdr);
-      // the stream's (probably) last batch is hashed here: nothing is left to overlap it with
-      if (end || short_read || (int64_t)job.n < kInlineMd5) m.update(job.p, job.n);
-      else w.submit(&job);
+      // the stream's (probably) last batch: nothing is left to overlap it with, so no hand-off to
+      // a scalar worker -- this thread, or an engine lane once the cores are all hashing
+      if ((int64_t)job.n < kInlineMd5) m.update(job.p, job.n);
+      else w.submit(&job, !(end || short_read));
       pc.mark(kHashInline);
     }
     if (end) {

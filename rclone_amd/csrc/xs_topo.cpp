@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rc_internal.h"
@@ -108,6 +109,35 @@ int parse_device_list(const char* s, std::vector<int>* out) {
   return (int)out->size();
 }
 
+// CPUs this process can use: its affinity mask, capped by the cgroup CPU quota (v2 cpu.max or v1
+// cpu.cfs_quota_us / cpu.cfs_period_us under the sysfs root); RCLONE_AMD_CPUS overrides.  A GPU
+// box share of 16 cores on a 256-CPU machine is 16, not 256.
+int effective_cpus() {
+  if (const char* e = getenv("RCLONE_AMD_CPUS")) {
+    const int v = atoi(e);
+    if (v > 0) return v;
+  }
+  int n = (int)std::thread::hardware_concurrency();
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+  double quota = -1;
+  std::string v;
+  const std::string root = sysfs_root();
+  if (read_line(root + "/fs/cgroup/cpu.max", &v)) {  // "max 100000" or "1600000 100000"
+    long long q = 0, per = 0;
+    if (sscanf(v.c_str(), "%lld %lld", &q, &per) == 2 && q > 0 && per > 0) quota = (double)q / (double)per;
+  } else {
+    std::string a, b;
+    if (read_line(root + "/fs/cgroup/cpu/cpu.cfs_quota_us", &a) && read_line(root + "/fs/cgroup/cpu/cpu.cfs_period_us", &b)) {
+      const long long q = atoll(a.c_str()), per = atoll(b.c_str());
+      if (q > 0 && per > 0) quota = (double)q / (double)per;
+    }
+  }
+  if (quota > 0) n = std::min(n, std::max(1, (int)(quota + 0.999)));
+  return std::max(1, n);
+}
+
 // Pin the calling thread to the CPUs of `node` (no-op when the node or its CPU list is unknown, or
 // RCLONE_AMD_NUMA=0).  Only threads this library starts are pinned -- never a caller's thread.
 void pin_thread_to_node(int node) {
@@ -154,6 +184,8 @@ extern "C" int xs_numa_node_cpus(int node, int* cpus, int cap) {
   for (int i = 0; i < cap && i < (int)v.size(); i++) cpus[i] = v[i];
   return (int)v.size();
 }
+
+extern "C" int xs_effective_cpus(void) { return xs::effective_cpus(); }
 
 extern "C" int xs_parse_device_list(const char* list, int* out, int cap) {
   std::vector<int> v;

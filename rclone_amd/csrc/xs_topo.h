@@ -10,6 +10,7 @@ bool parse_cpulist(const char* s, std::vector<int>* out);   // "0-15,32-47"
 bool node_cpus(int node, std::vector<int>* cpus);           // false when unknown / empty
 int parse_device_list(const char* s, std::vector<int>* out);
 bool numa_enabled();                                        // RCLONE_AMD_NUMA (default 1)
+int effective_cpus();  // affinity, capped by the cgroup CPU quota (RCLONE_AMD_CPUS overrides)
 void pin_thread_to_node(int node);                          // library-started threads only
 class ScopedMemPolicy {  // preferred-node policy of the calling thread while in scope
  public:

@@ -35,6 +35,7 @@
 #include "../../include/rclone_crypt_gpu.h"
 #include "../../rclone_amd/csrc/xs_host_md5.h"
 #include "../../rclone_amd/csrc/xs_topo.h"
+#include "../../rclone_amd/csrc/md5_workers.h"
 
 extern "C" {
 void orc_encrypt_file(uint8_t* out, const uint8_t* in, int64_t len, const uint8_t nonce0[24], const uint8_t key[32]);
@@ -732,6 +733,47 @@ static void test_topology() {
   (void)!system(("rm -rf " + r).c_str());
 }
 
+// ---------------------------------------------------------------- host MD5 tiers (md5_workers.h)
+// Many streams through one worker, a CPU budget of 1 and the 16-lane engine: jobs of odd sizes
+// (partial blocks on both ends), each stream's digest equal to the scalar MD5 of its bytes.
+static void test_md5_tiers() {
+  static xs::Md5Workers* w = new xs::Md5Workers(1, -1, 1, true);  // never destroyed (parked threads)
+  const uint64_t lanes0 = xs::md5_tier_stats().lanes.load();
+  std::atomic<int> bad{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < 24; t++)
+    th.emplace_back([&, t] {
+      uint64_t r = 0x9E37u * (t + 1);
+      auto rnd32 = [&] {
+        r = r * 6364136223846793005ull + 1442695040888963407ull;
+        return (uint32_t)(r >> 33);
+      };
+      std::vector<uint8_t> data(3 * 1048576 + 4096 * t + 7);
+      for (auto& b : data) b = (uint8_t)rnd32();
+      xs::HostMd5 got, want;
+      xs::Md5Job job;
+      job.st = &got;
+      size_t pos = 0;
+      while (pos < data.size()) {
+        const size_t n = std::min<size_t>(data.size() - pos, 1 + rnd32() % 300000);
+        md5_wait(&job);
+        job.p = data.data() + pos;
+        job.n = n;
+        w->submit(&job, (rnd32() & 1) != 0);
+        pos += n;
+      }
+      md5_wait(&job);
+      want.update(data.data(), data.size());
+      uint8_t a[16], b[16];
+      got.final(a);
+      want.final(b);
+      if (memcmp(a, b, 16)) bad++;
+    });
+  for (auto& x : th) x.join();
+  CHECK(bad == 0, "%d streams hashed wrongly through the tiers", bad.load());
+  CHECK(!xs::md5_x16_supported() || xs::md5_tier_stats().lanes.load() > lanes0, "engine lanes used");
+}
+
 // ---------------------------------------------------------------- concurrency (TSan)
 static void test_concurrency(rc_cipher* c, const uint8_t key[32]) {
   std::atomic<int> bad{0};
@@ -822,7 +864,9 @@ int main(int argc, char** argv) {
   rc_cipher_keys(c, key, nullptr, nullptr);
   if (only_concurrency) {
     test_concurrency(c, key);
+    test_md5_tiers();
   } else {
+    test_md5_tiers();
     test_concurrency(c, key);  // first: the decode tables are still unbuilt
     test_readahead(c);
     test_round_trips(c, key);

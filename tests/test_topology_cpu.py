@@ -67,3 +67,16 @@ def test_device_numa_node_without_device():
     # no HIP device here: unknown, never an error
     assert _lib.lib().xs_device_numa_node(0) == -1
     assert _lib.lib().xs_engine_numa_node(None) == -1
+
+
+def test_effective_cpus_follows_the_cgroup_quota(fake_sysfs, monkeypatch):
+    lib = _lib.lib()
+    aff = len(__import__("os").sched_getaffinity(0))
+    cg = fake_sysfs / "fs" / "cgroup"
+    cg.mkdir(parents=True)
+    (cg / "cpu.max").write_text("max 100000\n")  # no quota: the affinity mask
+    assert lib.xs_effective_cpus() == aff
+    (cg / "cpu.max").write_text("150000 100000\n")  # 1.5 CPUs of quota -> 2
+    assert lib.xs_effective_cpus() == min(aff, 2)
+    monkeypatch.setenv("RCLONE_AMD_CPUS", "5")
+    assert lib.xs_effective_cpus() == 5
