@@ -225,7 +225,10 @@ inline Md5Workers& md5_workers(int node) {
     if (const char* e = getenv("XS_MD5_WORKERS")) n = std::max(0, atoi(e));
     else n = std::max(1, std::min(8, cpus / 2));
     const char* l = getenv("XS_MD5_LANES");
-    w[slot] = new Md5Workers(n, slot - 1, cpus, l ? atoi(l) != 0 : true);
+    // scalar chains on host cores at once (workers + callers) before streams go to engine lanes
+    int budget = cpus;
+    if (const char* b = getenv("XS_MD5_SCALAR_BUDGET")) budget = std::max(1, atoi(b));
+    w[slot] = new Md5Workers(n, slot - 1, budget, l ? atoi(l) != 0 : true);
   }
   return *w[slot];
 }
