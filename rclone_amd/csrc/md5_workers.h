@@ -55,9 +55,11 @@ inline Md5TierStats& md5_tier_stats() {
 
 class Md5Workers {
  public:
-  Md5Workers(int max_threads, int node, int cpu_budget, bool lanes)
-      : max_(max_threads), node_(node), budget_(std::max(1, cpu_budget)), lanes_on_(lanes && md5_x16_supported()),
-        lane_threads_max_(std::max(1, cpu_budget / 8)) {}
+  // max_threads scalar workers; scalar_budget scalar chains on host cores at once before streams
+  // go to the engine; lane_threads engine threads at most (16 streams each).
+  Md5Workers(int max_threads, int node, int scalar_budget, bool lanes, int lane_threads)
+      : max_(max_threads), node_(node), budget_(std::max(1, scalar_budget)), lanes_on_(lanes && md5_x16_supported()),
+        lane_threads_max_(std::max(1, lane_threads)) {}
 
   // Hash j->st with j->p[0:n], here or later; the caller waits with wait() before touching j->st
   // or reusing j->p.  overlap: the caller has other work to do meanwhile (else a hand-off to a
@@ -228,7 +230,7 @@ inline Md5Workers& md5_workers(int node) {
     // scalar chains on host cores at once (workers + callers) before streams go to engine lanes
     int budget = cpus;
     if (const char* b = getenv("XS_MD5_SCALAR_BUDGET")) budget = std::max(1, atoi(b));
-    w[slot] = new Md5Workers(n, slot - 1, budget, l ? atoi(l) != 0 : true);
+    w[slot] = new Md5Workers(n, slot - 1, budget, l ? atoi(l) != 0 : true, std::max(1, cpus / 4));
   }
   return *w[slot];
 }

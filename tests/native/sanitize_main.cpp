@@ -737,7 +737,7 @@ static void test_topology() {
 // Many streams through one worker, a CPU budget of 1 and the 16-lane engine: jobs of odd sizes
 // (partial blocks on both ends), each stream's digest equal to the scalar MD5 of its bytes.
 static void test_md5_tiers() {
-  static xs::Md5Workers* w = new xs::Md5Workers(1, -1, 1, true);  // never destroyed (parked threads)
+  static xs::Md5Workers* w = new xs::Md5Workers(1, -1, 1, true, 2);  // never destroyed (parked threads)
   const uint64_t lanes0 = xs::md5_tier_stats().lanes.load();
   std::atomic<int> bad{0};
   std::vector<std::thread> th;
