@@ -149,3 +149,65 @@ def test_hash_errors_and_close():
     assert src.closes == 1
     want = hashlib.md5(orc.encrypt_file(plain, nonce, c.data_key)).hexdigest()
     assert c.compute_hash_with_nonce(nonce, _Closing(plain)) == want
+
+
+def _child_hash_tree(total, checkers):
+    """Run in a child process whose MD5 tiers are sized from its environment: per-object hashes
+    from `checkers` threads over a mixed tree, each checked against the oracle.  Prints one JSON
+    line (objects, mismatches, jobs per tier)."""
+    import ctypes
+    import json
+
+    from rclone_amd import _lib, crypt
+    c = crypt.Cipher("potato", "")
+    key = c.data_key
+    sizes = _tree(total, seed=0x1A9E)
+    bad, lock = [0], threading.Lock()
+    it = iter(range(len(sizes)))
+
+    def checker():
+        while True:
+            with lock:
+                i = next(it, None)
+            if i is None:
+                return
+            plain = splitmix64_bytes(0xC0000 + i, sizes[i])
+            nonce = splitmix64_bytes(0xD0000 + i, 24)
+            got = c.compute_hash_with_nonce(nonce, _Closing(plain))
+            if got != hashlib.md5(orc.encrypt_file(plain, nonce, key)).hexdigest():
+                with lock:
+                    bad[0] += 1
+
+    th = [threading.Thread(target=checker) for _ in range(checkers)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    print(json.dumps({"objects": len(sizes), "mismatches": bad[0], "cpus": _lib.lib().xs_effective_cpus()}))
+    del ctypes
+
+
+def test_per_object_hashes_through_engine_lanes():
+    # a CPU budget of 2 and one worker: most streams' MD5 runs in the 16-lane AVX-512 engine
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RCLONE_AMD_CPUS="2", XS_MD5_WORKERS="1", XS_MD5_SCALAR_BUDGET="1",
+               RCLONE_AMD_PHASES="1", PYTHONPATH=root)
+    code = "import tests.test_hash_stream_gpu as t; t._child_hash_tree(256 << 20, 16)"
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    phases = [json.loads(x)["rclone_amd_phases"] for x in r.stderr.splitlines() if x.startswith('{"rclone_amd_phases"')]
+    print(res, phases)
+    assert res["mismatches"] == 0 and res["objects"] > 200 and res["cpus"] == 2
+    assert phases and phases[-1]["md5_jobs_lanes"] > 0 or not _avx512()
+
+
+def _avx512():
+    try:
+        return "avx512f" in open("/proc/cpuinfo").read()
+    except OSError:
+        return False
