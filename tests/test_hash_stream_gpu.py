@@ -154,8 +154,7 @@ def test_hash_errors_and_close():
 def _child_hash_tree(total, checkers):
     """Run in a child process whose MD5 tiers are sized from its environment: per-object hashes
     from `checkers` threads over a mixed tree, each checked against the oracle.  Prints one JSON
-    line (objects, mismatches, jobs per tier)."""
-    import ctypes
+    line (objects, mismatches, the CPU budget seen)."""
     import json
 
     from rclone_amd import _lib, crypt
@@ -184,7 +183,6 @@ def _child_hash_tree(total, checkers):
     for t in th:
         t.join()
     print(json.dumps({"objects": len(sizes), "mismatches": bad[0], "cpus": _lib.lib().xs_effective_cpus()}))
-    del ctypes
 
 
 def test_per_object_hashes_through_engine_lanes():
