@@ -21,6 +21,8 @@
 // kernel launch, then the results are encoded and reassembled.  Outputs and errors (values
 // and which segment's error wins) are the reference's.
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
 #include <array>
 #include <atomic>
 #include <cctype>
@@ -678,15 +680,78 @@ struct SegBatch {
 constexpr size_t kChunkNames = 8192;
 constexpr unsigned kHostThreads = 16;
 
+// A batch's host stages call parallel_for three or four times; spawning 16 threads each time
+// costs milliseconds per call.  The helpers stay parked between calls (never destroyed).  One
+// batch uses them at a time; a concurrent batch spawns its own threads as before.
+class NamePool {
+ public:
+  explicit NamePool(unsigned helpers) {
+    for (unsigned t = 0; t < helpers; t++) th_.emplace_back([this] { run(); });
+  }
+  bool try_run(size_t n, const std::function<void(size_t)>& f) {
+    std::unique_lock<std::mutex> busy(use_, std::try_to_lock);
+    if (!busy.owns_lock()) return false;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      f_ = &f;
+      n_ = n;
+      next_.store(0);
+      active_ = (unsigned)th_.size();
+      gen_++;
+    }
+    cv_.notify_all();
+    for (size_t i; (i = next_.fetch_add(1)) < n;) f(i);  // the caller works too
+    std::unique_lock<std::mutex> g(mu_);
+    done_.wait(g, [&] { return active_ == 0; });
+    f_ = nullptr;
+    return true;
+  }
+  unsigned helpers() const { return (unsigned)th_.size(); }
+
+ private:
+  void run() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> g(mu_);
+    for (;;) {
+      cv_.wait(g, [&] { return gen_ != seen; });
+      seen = gen_;
+      const std::function<void(size_t)>* f = f_;
+      const size_t n = n_;
+      g.unlock();
+      for (size_t i; (i = next_.fetch_add(1)) < n;) (*f)(i);
+      g.lock();
+      if (--active_ == 0) done_.notify_one();
+    }
+  }
+  std::mutex use_, mu_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> th_;
+  const std::function<void(size_t)>* f_ = nullptr;
+  size_t n_ = 0;
+  std::atomic<size_t> next_{0};
+  unsigned active_ = 0;
+  uint64_t gen_ = 0;
+};
+
+unsigned name_threads() {
+  static const unsigned nt = [] {
+    unsigned v = (unsigned)xs::effective_cpus();
+    if (const char* e = getenv("RCLONE_AMD_NAME_THREADS")) v = (unsigned)atoi(e);
+    return std::max(1u, std::min(v, kHostThreads));
+  }();
+  return nt;
+}
+
 template <class F>
 void parallel_for(size_t n, F f) {
-  unsigned nt = std::thread::hardware_concurrency();
-  if (const char* e = getenv("RCLONE_AMD_NAME_THREADS")) nt = (unsigned)atoi(e);
-  nt = std::max(1u, std::min({nt, kHostThreads, (unsigned)n}));
+  const unsigned nt = std::max(1u, std::min(name_threads(), (unsigned)n));
   if (nt <= 1) {
     for (size_t i = 0; i < n; i++) f(i);
     return;
   }
+  static NamePool* pool = new NamePool(name_threads() - 1);
+  const std::function<void(size_t)> fn = f;
+  if (pool->helpers() + 1 >= nt && pool->try_run(n, fn)) return;
   std::atomic<size_t> next{0};
   std::vector<std::thread> th;
   for (unsigned t = 0; t < nt; t++)
