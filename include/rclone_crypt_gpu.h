@@ -48,7 +48,8 @@ extern "C" {
  * base pointers.  Seal: src_off -> plaintext, dst_off -> wire block (tag first).
  * Open: src_off -> wire block (tag first), dst_off -> plaintext.  len = plaintext bytes
  * (1..65536).  Payload addresses (plaintext and ciphertext = wire + 16) must be 16-byte
- * aligned. */
+ * aligned.  reserved: 0 (the engine uses it internally for ranged opens; the *_batch_dev entry
+ * points ignore it). */
 typedef struct xs_block_desc {
   uint64_t src_off;
   uint64_t dst_off;
@@ -154,6 +155,15 @@ int xs_engine_seal(xs_engine *e, const uint8_t key[32], const uint8_t nonce0[24]
  * thread while the call runs. */
 int xs_engine_open(xs_engine *e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
                    const void *body, uint64_t body_len, void *plain, uint8_t *ok);
+/* xs_engine_open for a caller that will read only plaintext bytes [range_lo, range_hi) of
+ * `plain` (offsets within this call's plaintext): the decrypter after RangeSeek with a limit
+ * (cipher.go:972-1034), whose reads stop at offset + limit.  Every block's tag is verified over the
+ * whole block and ok[] is as for xs_engine_open, but bytes of `plain` outside the range may be
+ * left unwritten: a ranged 4 KiB read then decrypts one or two 4 KiB groups of its block instead
+ * of all sixteen.  A failed block is zero-filled whole, as before. */
+int xs_engine_open_range(xs_engine *e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                         const void *body, uint64_t body_len, void *plain, uint8_t *ok, uint64_t range_lo,
+                         uint64_t range_hi);
 /* Seal many host objects and MD5 their crypt files on the GPU -- the hash Fs.put tees off the
  * ciphertext (crypt.go:516-533) and cryptcheck's computeHashWithNonce (crypt.go:784-806),
  * batched across objects: object i = plain[offs[i] : offs[i]+lens[i]] (offs 16-byte aligned),

@@ -63,6 +63,7 @@ _SIGS = [
     ("xs_engine_destroy", None, [vp]),
     ("xs_engine_seal", ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, u64, vp, u64, vp]),
     ("xs_engine_open", ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, u64, vp, u64, vp, vp]),
+    ("xs_engine_open_range", ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, u64, vp, u64, vp, vp, u64, u64]),
     ("xs_engine_seal_md5", ctypes.c_int, [vp, ctypes.c_char_p, u64, vp, vp, vp, vp, vp]),
     ("xs_engine_put_batch", ctypes.c_int, [vp, ctypes.c_char_p, u64, vp, vp, vp, vp, vp, vp]),
     ("xs_put_body_bytes", u64, [u64, vp]),

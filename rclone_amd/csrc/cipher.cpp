@@ -629,6 +629,9 @@ struct rc_decrypter {
   int32_t err = RC_NIL;
   bool finished = false;
   int64_t limit = -1;
+  // plaintext offset, from the next batch's start, of the first byte a Read can reach: the
+  // discard of the RangeSeek that fills that batch (bytes before it are never served)
+  int64_t win_lo = 0;
   rc_open_fn open = nullptr;
   void* open_user = nullptr;
   int32_t wrapped = RC_NIL;
@@ -713,8 +716,13 @@ static int32_t dec_read_batch(rc_decrypter* fh, uint32_t want) {
   fh->nblk = nb;
   if (nb == 0) return RC_NIL;
   fh->grow = grow_batch(fh->c, ra, total, std::chrono::steady_clock::now() - t0);
-  if (xs_engine_open(fh->eng, fh->c->data_key, fh->nonce, 0, fh->wire.p, (uint64_t)total, fh->plain.p,
-                                 fh->okb.p) != XS_OK) {
+  // Reads reach plaintext bytes [win_lo, limit) of this batch at most (limit counts from the batch
+  // start here, see range_seek_locked): the GPU may skip decrypting the rest of a block, every tag
+  // is still verified whole (a ranged 4 KiB read decrypts one or two 4 KiB groups of its block)
+  const uint64_t lo = (uint64_t)fh->win_lo, hi = fh->limit >= 0 ? (uint64_t)fh->limit : UINT64_MAX;
+  fh->win_lo = 0;
+  if (xs_engine_open_range(fh->eng, fh->c->data_key, fh->nonce, 0, fh->wire.p, (uint64_t)total, fh->plain.p,
+                           fh->okb.p, lo, hi) != XS_OK) {
     fh->nblk = 0;
     return RC_ERR_GPU;
   }
@@ -920,9 +928,12 @@ static int64_t range_seek_locked(rc_decrypter* fh, int64_t offset, int32_t whenc
     fh->rc = nrc;
     fh->have_rc = true;
   }
-  // fillBuffer for the first block; read ahead only what (discard + limit) needs
+  // fillBuffer for the first block; read ahead only what (discard + limit) needs, and decrypt only
+  // what Reads from discard on can reach
   fh->limit = (limit >= 0) ? discard + limit : -1;
+  fh->win_lo = discard;
   int32_t e = dec_fill(fh);
+  fh->win_lo = 0;
   if (e != RC_NIL) {
     *err = dec_finish(fh, e);
     return 0;

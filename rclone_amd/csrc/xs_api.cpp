@@ -368,6 +368,9 @@ struct xs_engine {
     bool zc;
     uint64_t d_in, d_out;
     uint64_t blk0;  // first block within its combined batch
+    // OPEN: the plaintext bytes [range_lo, range_hi) of out the caller will read (xs_engine_open_range);
+    // the fused kernel leaves the rest of a full block's 4 KiB groups undecrypted
+    uint64_t range_lo, range_hi;
     // woken (under qmu) when the request is done or when it heads the queue and the lead is free:
     // one waiter at a time, not every caller on each completion
     std::condition_variable cv;
@@ -616,7 +619,8 @@ static int engine_sync(xs_engine* e) {
 }
 
 static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
-                         const void* in, uint64_t in_len, void* out, uint8_t* ok, uint64_t nblocks);
+                         const void* in, uint64_t in_len, void* out, uint8_t* ok, uint64_t nblocks, uint64_t range_lo = 0,
+                         uint64_t range_hi = UINT64_MAX);
 
 static int engine_seal_direct(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
                               const void* plain, uint64_t plain_len, void* body);
@@ -676,6 +680,41 @@ static int engine_seal_direct(xs_engine* e, const uint8_t key[32], const uint8_t
     if (err != hipSuccess) return hip_fail(err, "D2H");
   }
   return engine_sync(e);
+}
+
+// The descriptor's group window for block j of an OPEN request whose caller reads only plaintext
+// bytes [lo, hi): 0 = the whole block, else XS_DESC_WINDOW | one bit per 4 KiB group to decrypt.
+// Group g is keystream blocks 64g..64g+63, i.e. plaintext bytes [4096g - 32, 4096g + 4064) of the
+// block (keystream block 0's first 32 bytes are the Poly1305 key); the last 32 bytes (keystream
+// block 1024) are always written.
+static uint32_t open_window(uint64_t lo, uint64_t hi, uint64_t j) {
+  const uint64_t b0 = j * XS_BLOCK_DATA, b1 = b0 + XS_BLOCK_DATA;
+  if (lo <= b0 && hi >= b1) return 0u;
+  uint32_t mask = 0;
+  if (lo < b1 && hi > b0 && hi > lo) {
+    const uint64_t a = std::max(lo, b0) - b0, z = std::min(hi, b1) - b0;  // [a, z) within the block
+    const uint64_t g0 = (a + 32) / XS_WINDOW_GROUP, g1 = std::min<uint64_t>((z - 1 + 32) / XS_WINDOW_GROUP, 15);
+    for (uint64_t g = g0; g <= g1; g++) mask |= 1u << g;
+  }
+  return XS_DESC_WINDOW | mask;
+}
+
+extern "C" int xs_engine_open_range(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                                    const void* body, uint64_t body_len, void* plain, uint8_t* ok, uint64_t range_lo,
+                                    uint64_t range_hi) {
+  if (!e || !key || !nonce0 || (body_len && (!body || !plain || !ok))) {
+    set_error("xs_engine_open_range: null argument");
+    return XS_ERR_INVALID;
+  }
+  if (body_len == 0) return XS_OK;
+  const uint64_t nblocks = (body_len + XS_BLOCK_SIZE - 1) / XS_BLOCK_SIZE;
+  if (body_len - (nblocks - 1) * XS_BLOCK_SIZE <= XS_BLOCK_HDR) {
+    set_error("xs_engine_open_range: truncated block header");
+    return XS_ERR_INVALID;
+  }
+  if (e->coalesce && nblocks <= e->c_cap_blocks)
+    return engine_submit(e, false, key, nonce0, first_block, body, body_len, plain, ok, nblocks, range_lo, range_hi);
+  return engine_open_direct(e, key, nonce0, first_block, body, body_len, plain, ok);  // writes every byte
 }
 
 extern "C" int xs_engine_open(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
@@ -878,7 +917,7 @@ static int engine_issue_batch(xs_engine* e, xs_engine::CSlot& c) {
     outoff[r] = out_pos;
     for (uint64_t j = 0; j < q->nblocks; j++) {
       xs_block_desc& d = c.h_desc[nblk + j];
-      d.reserved = 0;
+      d.reserved = q->seal ? 0u : open_window(q->range_lo, q->range_hi, j);
       nonce_plus(d.nonce, q->nonce0, q->first_block + j);
       if (q->seal) {
         d.src_off = in_pos + j * XS_BLOCK_DATA;
@@ -968,9 +1007,12 @@ static void engine_wait_batch(xs_engine::CSlot& c) {
 }
 
 static int engine_submit(xs_engine* e, bool seal, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
-                         const void* in, uint64_t in_len, void* out, uint8_t* ok, uint64_t nblocks) {
+                         const void* in, uint64_t in_len, void* out, uint8_t* ok, uint64_t nblocks, uint64_t range_lo,
+                         uint64_t range_hi) {
   xs_engine::Req req{};
   req.seal = seal;
+  req.range_lo = range_lo;
+  req.range_hi = range_hi;
   memcpy(req.key, key, 32);
   memcpy(req.nonce0, nonce0, 24);
   req.first_block = first_block;

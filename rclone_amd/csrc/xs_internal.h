@@ -59,6 +59,14 @@ hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const
 // (optional): the same descriptors in host memory; batches of <= XS_INLINE_DESCS blocks then travel
 // in the kernel arguments and the kernel does not read desc over PCIe (v2 / v3).
 constexpr int XS_INLINE_DESCS = 16;
+// OPEN descriptors built by the engine for a ranged read (xs_engine_open_range) carry a group
+// window in xs_block_desc.reserved: 0 = decrypt the whole block; XS_DESC_WINDOW | mask = decrypt
+// only the 4 KiB groups g with bit g of mask set (the tag is verified over the whole block either
+// way).  Group g is keystream blocks 64g..64g+63 = plaintext bytes [4096g - 32, 4096g + 4064); the
+// block's last 32 bytes (keystream block 1024) are always written.  Only the fused v2 / v3
+// kernels act on it (full blocks); every other path writes all bytes.
+constexpr uint32_t XS_DESC_WINDOW = 0x80000000u;
+constexpr uint64_t XS_WINDOW_GROUP = 4096;
 struct XsInlineDescs {
   xs_block_desc d[XS_INLINE_DESCS];
   uint32_t n;  // d[0..n) valid; blocks >= n read desc

@@ -622,85 +622,6 @@ __device__ void full_corr(bool seal, P5 sumA, P5 sumB, P5 sumC, P5 sumD4, const 
   put5(o->corr, c);
 }
 
-// full_corr spread over the lanes of one wave (keygen_wave, latency): lanes 0..3 form the four
-// table sums at once, then the three independent product chains of corr -- S (lane 0), E*SW - B
-// (lane 1) and 2^128 (r^65 + r^66) [+ the SEAL key-slot words] times W63 (lane 2; lanes 3, 4 the
-// key-slot products) -- run in the same instructions; lane 0 combines.  pw[l] holds lane l's
-// table entry (C = lanes 0..7, D = 9..17, A = 18..25, B = 27..34, W63 = 36, r^65 = 37, r^66 = 38).
-// Same operations and canonicalisations as full_corr, so corr is bit-identical.
-__device__ __forceinline__ P5 shfl5(const P5& v, uint32_t src) {
-  P5 o;
-#pragma unroll
-  for (int i = 0; i < 5; i++) o.v[i] = (uint32_t)__shfl((int)v.v[i], (int)src);
-  return o;
-}
-__device__ __forceinline__ P5 sel5(bool c, const P5& a, const P5& b) {
-  P5 o;
-#pragma unroll
-  for (int i = 0; i < 5; i++) o.v[i] = c ? a.v[i] : b.v[i];
-  return o;
-}
-__device__ __forceinline__ P5 lds5(const uint32_t (*pw)[5], uint32_t k) {
-  P5 o;
-#pragma unroll
-  for (int i = 0; i < 5; i++) o.v[i] = pw[k][i];
-  return o;
-}
-
-__device__ __forceinline__ void full_corr_wave(bool seal, uint32_t l, const uint32_t (*pw)[5], const uint32_t (&ks)[16],
-                                               BlockKey* __restrict__ o) {
-  // table sums: lane 0 sum C, lane 1 sum A, lane 2 sum B, lane 3 D0..D3
-  const uint32_t base = l == 0u ? 0u : l == 1u ? 18u : l == 2u ? 27u : 9u;
-  const uint32_t cnt = l == 3u ? 4u : 8u;
-  P5 sum;
-#pragma unroll
-  for (int i = 0; i < 5; i++) sum.v[i] = 0;
-  if (l < 4u) {
-#pragma unroll
-    for (uint32_t k = 0; k < 8; k++)
-      if (k < cnt) add5(sum, lds5(pw, base + k));
-  }
-  pnorm(sum);
-  const P5 sumB = shfl5(sum, 2u), sumD4 = shfl5(sum, 3u);
-  const P5 r3 = lds5(pw, 3), r32 = lds5(pw, 13), W63 = lds5(pw, 36), r65 = lds5(pw, 37), r66 = lds5(pw, 38);
-  P5 E, B, two128, r6566 = r65;
-#pragma unroll
-  for (int i = 0; i < 5; i++) {
-    E.v[i] = kE[i];
-    B.v[i] = kB[i];
-    two128.v[i] = 0;
-  }
-  two128.v[4] = 1u << 24;  // 2^128 = 2^(104 + 24)
-  add5(r6566, r66);
-  pnorm(r6566);
-  // step 1: r3*sumC | sumA*sumB | 2^128 (r65 + r66) | key slot lo * r66 | key slot hi * r65
-  P5 x = sel5(l == 0u, r3, sel5(l == 1u, sum, sel5(l == 2u, two128, sel5(l == 3u, chunk26(ks[0], ks[1], ks[2], ks[3]),
-                                                                               chunk26(ks[4], ks[5], ks[6], ks[7])))));
-  P5 y = sel5(l == 0u, sum, sel5(l == 1u, sumB, sel5(l == 2u, r6566, sel5(l == 3u, r66, r65))));
-  P5 t = pmul(x, y);
-  // step 2: (r3 sumC) sumD4 | E * SW | kk * W63
-  const P5 t3 = shfl5(t, 3u), t4 = shfl5(t, 4u);
-  P5 kk = t;
-  if (seal) {
-    add5(kk, t3);
-    add5(kk, t4);
-    pnorm(kk);
-  }
-  x = sel5(l == 0u, t, sel5(l == 1u, E, kk));
-  y = sel5(l == 0u, sumD4, sel5(l == 1u, pcanon(t), W63));
-  t = pmul(x, y);
-  // step 3: S = (..) (1 + r^32) on lane 0; es_b (lane 1) and b (lane 2) canonicalised
-  P5 one_r32 = r32;
-  one_r32.v[0] += 1;
-  const P5 es_b = pcanon(psub(pcanon(t), B));
-  const P5 bb = pcanon(t);
-  const P5 S = pcanon(pmul(t, one_r32));
-  // step 4: a = S * es_b, corr = a - b
-  const P5 a = pcanon(pmul(S, shfl5(es_b, 1u)));
-  const P5 c = pcanon(psub(a, shfl5(bb, 2u)));
-  if (l == 0u) put5(o->corr, c);
-}
-
 // ---------------------------------------------------------------- keygen
 // One lane per crypt block.  MODE: 0 object seal, 1 object open, 2 descriptor seal,
 // 3 descriptor open.  Object mode derives nonce, offsets and length from the block
@@ -847,13 +768,14 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
 // lanes of a wave share one block: lanes < 32 make keystream block 0 while lanes >= 32 make
 // block 1024 (one Salsa20 latency instead of two), and the table entries are built across
 // lanes (a wave issues one pmul for all lanes at once): full blocks in 13 pmul steps (levels
-// of base^0..base^8 for the bases r, r^8, r^64, r^512, three steps each, then W_63, r^65, r^66)
+// of base^0..base^8 for the bases r, r^8, r^64, r^512, three steps each, spare lanes building
+// the correction term's products in the same instructions, then one step for r^3 and r^4096)
 // instead of the ~45 of full_tables' chains; partial blocks (lane 0..31 T1[i] = r^i, 32..39
 // T2[a] = r^(32a), 40 R = r^253) by square-and-multiply per lane, 8 steps.  The entries are
 // other representatives of the same residues (pmul-bounded, as the crypt kernels accept); corr
 // is canonical, so tags and ciphertext equal the narrow keygen's.
 // The body: one wave (lanes l = threadIdx.x & 63) builds block b's key schedule into *o (global
-// memory, or LDS in the fused kernels); pw = 64 x 5 words of LDS scratch private to the wave.
+// memory, or LDS in the fused kernels).
 #ifdef XS_F2_PROBE
 extern __device__ unsigned long long xs_f2_probe[2 * 10 * 16];
 #define KG_MARK(slot)                                                                              \
@@ -883,10 +805,12 @@ __device__ __forceinline__ void lds_wait_flag(const uint32_t* flag) {
   }
 }
 // Raise *flag (LDS) once this wave's earlier LDS writes have completed.  Not a release: that would
-// also wait for the wave's outstanding global loads (vmcnt), the PCIe round trip here.
+// also wait for the wave's outstanding global loads (vmcnt), the PCIe round trip here.  Inline
+// ds_write for the same reason as the reads above: a compiler-visible store to LDS (even a relaxed
+// atomic) gets a vmcnt(0) first, since the wave's LDS-DMA loads might target the same word.
 __device__ __forceinline__ void lds_raise_flag(uint32_t* flag) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const uint32_t fa = (uint32_t)(uintptr_t)(lds_u32*)flag;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\tds_write_b32 %0, %1" : : "v"(fa), "v"(1u) : "memory");
 }
 __device__ __forceinline__ void lds_wait_subkey(const uint32_t* flag, const uint32_t* sk, uint32_t out[8]) {
   const uint32_t ka = (uint32_t)(uintptr_t)(const lds_u32*)sk;
@@ -903,8 +827,9 @@ struct KgNoMid {
 };
 template <int MODE, class Mid = KgNoMid>
 __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32_t n[6], uint64_t src, uint64_t dst,
-                                                 uint32_t len, BlockKey* o, uint32_t (*pw)[5], const uint32_t* sk_lds,
-                                                 const uint32_t* sk_flag, const Mid& mid = Mid());
+                                                 uint32_t len, BlockKey* o, const uint32_t* sk_lds,
+                                                 const uint32_t* sk_flag, const Mid& mid = Mid(),
+                                                 uint32_t* cd_flag = nullptr);
 
 // sk_lds / sk_flag (LDS, optional): take the HSalsa20 subkey another wave of the workgroup derives
 // for the same block (its LDS writes completed, then *sk_flag raised) instead of computing it
@@ -912,7 +837,7 @@ __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32
 template <int MODE>
 __device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& nonce0, uint64_t first_block,
                                             uint64_t total_len, const xs_block_desc* __restrict__ desc,
-                                            uint64_t b, BlockKey* o, uint32_t (*pw)[5],
+                                            uint64_t b, BlockKey* o,
                                             const uint32_t* sk_lds = nullptr, const uint32_t* sk_flag = nullptr) {
   const uint32_t l = threadIdx.x & 63u;
   uint32_t n[6];
@@ -925,7 +850,7 @@ __device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& n
     }
     return;
   }
-  keygen_wave_body<MODE>(key, n, src, dst, len, o, pw, sk_lds, sk_flag);
+  keygen_wave_body<MODE>(key, n, src, dst, len, o, sk_lds, sk_flag);
 }
 
 // The key schedule of one block whose descriptor fields are already known (and valid).  For a
@@ -933,8 +858,8 @@ __device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& n
 // term): the fused kernel builds its Toeplitz table there and lets the crypt waves go on.
 template <int MODE, class Mid>
 __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32_t n[6], uint64_t src, uint64_t dst,
-                                                 uint32_t len, BlockKey* o, uint32_t (*pw)[5], const uint32_t* sk_lds,
-                                                 const uint32_t* sk_flag, const Mid& mid) {
+                                                 uint32_t len, BlockKey* o, const uint32_t* sk_lds,
+                                                 const uint32_t* sk_flag, const Mid& mid, uint32_t* cd_flag) {
   const uint32_t l = threadIdx.x & 63u;
   uint32_t sk[8];
   KG_MARK(0);
@@ -984,7 +909,34 @@ __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32
   if (len == XS_BLOCK_DATA) {
     // Level m = 0..3 (bases r, r^8, r^64, r^512) lives in lanes 9m + b holding base^b,
     // b = 0..8; three pmul steps per level (b = 2; 3, 4; 5..8), lane 9m + 8 = the next base.
+    // Step st of level m multiplies by base^(2^st) = r^(2^(3m + st)): over the 12 steps these are
+    // r^1, r^2, ..., r^2048, the factors of the correction term's product forms (full_corr):
+    //   sum C (1 + r^32) sum D4 = prod_{i<6} (1 + r^(2^i)),  sum A sum B = prod_{6<=i<12} (1 + r^(2^i)),
+    // so  corr = E r^3 prod_{i<12} (1 + r^(2^i)) - B r^3 prod_{i<6} (1 + r^(2^i)) - K,
+    //   K = 2^128 (r^65 + r^66) W_63 [+ SEAL key slots] = r^4096 ((2^128 [+ ks_lo]) r^2 + (2^128 [+ ks_hi]) r).
+    // Spare lanes ride along in the same pmul instructions: lane 40 accumulates the E product
+    // (all 12 steps), lane 41 the B product (steps 0..5), lanes 42 / 43 the two K terms (steps
+    // 1 / 0).  One more step after the levels multiplies in r^3 (lanes 40, 41) and r^4096 (lane 42);
+    // then corr is two subtractions and one canonicalisation instead of a chain of products.
+    constexpr uint32_t kLaneE = 40u, kLaneB = 41u, kLaneKlo = 42u, kLaneKhi = 43u;
+    const bool seal = MODE == 0 || MODE == 2;
+    P5 two128;
+#pragma unroll
+    for (int i = 0; i < 5; i++) two128.v[i] = 0;
+    two128.v[4] = 1u << 24;  // 2^128 = 2^(104 + 24)
     if (l == 1) p = r;
+    if (l == kLaneE) {
+#pragma unroll
+      for (int i = 0; i < 5; i++) p.v[i] = kE[i];
+    } else if (l == kLaneB) {
+#pragma unroll
+      for (int i = 0; i < 5; i++) p.v[i] = kB[i];
+    } else if (l == kLaneKlo || l == kLaneKhi) {
+      p = two128;
+      if (seal) {  // the key-slot words (chunk -2 = ks[0..3], chunk -1 = ks[4..7])
+        add5(p, l == kLaneKlo ? chunk26(ks[0], ks[1], ks[2], ks[3]) : chunk26(ks[4], ks[5], ks[6], ks[7]));
+      }
+    }
 #pragma unroll
     for (int m = 0; m < 4; m++) {
       const uint32_t b = l - 9u * m;  // wraps for lanes below the level: not in 2..8
@@ -993,18 +945,37 @@ __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32
         // operands: st 0: b=2 <- 1*1; st 1: b=3 <- 2*1, b=4 <- 2*2; st 2: b=5..8 <- 4*(b-4)
         const uint32_t lo = st == 0 ? 2u : st == 1 ? 3u : 5u, hi = st == 0 ? 2u : st == 1 ? 4u : 8u;
         const bool act = b >= lo && b <= hi;
+        const int step = 3 * m + st;
+        // spare lanes multiply their own value by the step's factor: (1 + a) or a
+        const bool plus1 = l == kLaneE || (l == kLaneB && step < 6);
+        const bool own = plus1 || (l == kLaneKlo && step == 1) || (l == kLaneKhi && step == 0);
         const uint32_t ia = 9u * m + (st == 0 ? 1u : st == 1 ? 2u : 4u);
-        const uint32_t ib = 9u * m + (act ? (st == 0 ? 1u : st == 1 ? b - 2u : b - 4u) : 0u);
+        const uint32_t ib = own ? l : 9u * m + (act ? (st == 0 ? 1u : st == 1 ? b - 2u : b - 4u) : 0u);
         P5 a, c;
 #pragma unroll
         for (int i = 0; i < 5; i++) {
           a.v[i] = (uint32_t)__shfl((int)p.v[i], (int)ia);
           c.v[i] = (uint32_t)__shfl((int)p.v[i], (int)ib);
         }
+        a.v[0] += plus1 ? 1u : 0u;
         const P5 q = pmul(a, c);
-        if (act) p = q;
+        if (act || own) p = q;
       }
       KG_MARK(3 + m);
+      if (m == 1) {  // C[b] = lane b, D[a] = lane 9 + a are final: out now (cd_flag: LDS, raised after)
+        if (l < 8) put5(o->full.C[l], p);
+        else if (l >= 9 && l < 18) put5(o->full.D[l - 9], p);
+        if (cd_flag) lds_raise_flag(cd_flag);
+      }
+      if (m == 0) {  // K = r^4096 (lane 42 + lane 43), summed in lane 42
+        P5 khi;
+#pragma unroll
+        for (int i = 0; i < 5; i++) khi.v[i] = (uint32_t)__shfl((int)p.v[i], (int)kLaneKhi);
+        if (l == kLaneKlo) {
+          add5(p, khi);
+          pnorm(p);
+        }
+      }
       if (m < 3) {  // next level: base^0 = 1, base^1 = this level's base^8
         P5 nb;
 #pragma unroll
@@ -1012,33 +983,31 @@ __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32
         if (l == 9u * (m + 1) + 1u) p = nb;
       }
     }
-    // C[b] = lane b, D[a] = lane 9 + a, A[i] = lane 18 + i, B[j] = lane 27 + j;
-    // lane 36: W63 = A[7] B[7] = r^4032, lane 37: r^65 = A[1] C[1], lane 38: r^66 = A[1] C[2]
+    // A[i] = lane 18 + i, B[j] = lane 27 + j
     if (l >= 18 && l < 26) put5(o->full.A[l - 18], p);
     else if (l >= 27 && l < 35) put5(o->full.B[l - 27], p);
     mid();
-    {
-      const uint32_t ia = l == 36u ? 25u : 19u, ib = l == 36u ? 34u : l == 37u ? 1u : 2u;
-      P5 a, c;
+    {  // r^3 (lane 3) into lanes 40, 41; r^4096 (lane 35) into lane 42
+      const uint32_t ia = l == kLaneKlo ? 35u : 3u;
+      P5 a;
 #pragma unroll
-      for (int i = 0; i < 5; i++) {
-        a.v[i] = (uint32_t)__shfl((int)p.v[i], (int)ia);
-        c.v[i] = (uint32_t)__shfl((int)p.v[i], (int)ib);
-      }
-      const P5 q = pmul(a, c);
-      if (l >= 36u && l <= 38u) p = q;
+      for (int i = 0; i < 5; i++) a.v[i] = (uint32_t)__shfl((int)p.v[i], (int)ia);
+      const P5 q = pmul(a, p);
+      if (l >= kLaneE && l <= kLaneKlo) p = q;
     }
     KG_MARK(7);
-    if (l < 8) put5(o->full.C[l], p);
-    else if (l >= 9 && l < 18) put5(o->full.D[l - 9], p);
+    P5 e, bq, k;
 #pragma unroll
-    for (int i = 0; i < 5; i++) pw[l][i] = p.v[i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    KG_MARK(8);
-    full_corr_wave(MODE == 0 || MODE == 2, l, pw, ks, o);
+    for (int i = 0; i < 5; i++) {
+      e.v[i] = as_varying(__builtin_amdgcn_readlane(p.v[i], kLaneE));
+      bq.v[i] = as_varying(__builtin_amdgcn_readlane(p.v[i], kLaneB));
+      k.v[i] = as_varying(__builtin_amdgcn_readlane(p.v[i], kLaneKlo));
+    }
+    // pmul outputs (limbs < 2^26 + 2^6) are valid subtrahends for psub; corr is canonical, the
+    // same value full_corr gives
+    const P5 cr = pcanon(psub(psub(e, bq), k));
     KG_MARK(9);
+    if (l == 0) put5(o->corr, cr);
     return;
   }
   // partial blocks (one per object at most): lane e's entry by square-and-multiply
@@ -1060,9 +1029,8 @@ __global__ void __launch_bounds__(64) xs_keygen_wide(KeyArg key, NonceArg nonce0
                                                      uint64_t total_len, uint64_t nblocks,
                                                      const xs_block_desc* __restrict__ desc,
                                                      BlockKey* __restrict__ out) {
-  __shared__ uint32_t pw[64][5];
   if (blockIdx.x >= nblocks) return;  // uniform per workgroup
-  keygen_wave<MODE>(key, nonce0, first_block, total_len, desc, blockIdx.x, out + blockIdx.x, pw);
+  keygen_wave<MODE>(key, nonce0, first_block, total_len, desc, blockIdx.x, out + blockIdx.x);
 }
 
 // ---------------------------------------------------------------- main block kernel
@@ -1772,9 +1740,8 @@ __global__ void __launch_bounds__(256) xs_crypt_fused(KeyArg key, NonceArg bound
                                                       uint32_t seq) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
   __shared__ BlockKey kl;
-  __shared__ uint32_t pw[64][5];
   if (blockIdx.x >= nblocks) return;  // uniform per workgroup (grid == nblocks)
-  if (threadIdx.x < 64) keygen_wave<SEAL ? 2 : 3>(key, bounds, 0, 0, desc, blockIdx.x, &kl, pw);
+  if (threadIdx.x < 64) keygen_wave<SEAL ? 2 : 3>(key, bounds, 0, 0, desc, blockIdx.x, &kl);
   __syncthreads();
   crypt_wave<SEAL, 4, true>(&kl, nblocks, src, dst, ok, lds);
   if (ctr) xs_fused_complete(ctr, flag, seq, nblocks);
@@ -1823,6 +1790,34 @@ constexpr int f2_max_groups() { return NCW == 4 ? 5 : XS_F3_DIST ? 2 : 3; }
 template <int NCW>
 constexpr int f2_lds_words() { return 16 * 1024 + NCW * 1024 + (NCW - 1) * 2048 + 64 * 12; }
 
+// Sum of a P5 over the 64 lanes of a wave, left in every lane, without LDS round trips: quad DPP
+// (lanes l ^ 1, l ^ 2), row half-mirror and mirror (the other quad of 8 lanes, the other 8 of a
+// 16-lane row: the partial sums are uniform within those groups by then), v_permlane16_swap (the
+// other row of a 32-lane half) and v_permlane32_swap (the other half).  Limbs come in pnorm-bounded
+// (< 2^26 + 2^6); one pnorm after 32 lanes keeps every limb below 2^32.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ void wave_sum5(P5& h) {
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    uint32_t v = h.v[i];
+    v += dpp_u32<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+    v += dpp_u32<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+    v += dpp_u32<0x141>(v);  // row_half_mirror
+    v += dpp_u32<0x140>(v);  // row_mirror
+    const auto s16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    h.v[i] = s16[0] + s16[1];
+  }
+  pnorm(h);
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const auto s32 = __builtin_amdgcn_permlane32_swap(h.v[i], h.v[i], false, false);
+    h.v[i] = s32[0] + s32[1];
+  }
+}
+
 #ifdef XS_F2_PROBE
 // Diagnostic build only (tools/fused_probe.cpp): s_memrealtime (100 MHz) at phase boundaries, per
 // wave of workgroup 0, lane-indexed vector stores.
@@ -1850,13 +1845,13 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
   static_assert(f2_lds_words<NCW>() >= LDS_WORDS, "the fallback path runs crypt_wave in this LDS");
   __shared__ __attribute__((aligned(16))) uint32_t lds[f2_lds_words<NCW>()];
   __shared__ BlockKey kl;
-  __shared__ uint32_t pw[64][5];
-  // hs_flag[0..3]: subkeys of waves 0..3 published (for waves 4..7 / the key wave); [4]: Z table ready
-  __shared__ uint32_t hs_key[4][8], hs_flag[5];
+  // hs_flag[0..3]: subkeys of waves 0..3 published (for waves 4..7 / the key wave); [4]: Z table ready;
+  // [5]: C and D power tables in kl (wave 0's finalisation factor)
+  __shared__ uint32_t hs_key[4][8], hs_flag[6];
   if (blockIdx.x >= nblocks) return;  // uniform per workgroup (grid == nblocks)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63u;
   const uint64_t blk = blockIdx.x;
-  if (threadIdx.x < 5u) hs_flag[threadIdx.x] = 0u;
+  if (threadIdx.x < 6u) hs_flag[threadIdx.x] = 0u;
   F2_MARK(0);
   uint32_t nn[6];
   uint64_t soff, doff;
@@ -1876,13 +1871,20 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
   doff = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(doff >> 32)) << 32) |
          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)doff);
   len = __builtin_amdgcn_readfirstlane(len);
+  // OPEN of a ranged read: decrypt only the 4 KiB groups the caller reads (XS_DESC_WINDOW)
+  uint32_t gwin = 0xFFFFu;
+  if (!SEAL) {
+    const uint32_t rsv = blk < inl.n ? inl.d[blk].reserved : desc[blk].reserved;
+    if (rsv & XS_DESC_WINDOW) gwin = rsv & 0xFFFFu;
+  }
+  gwin = __builtin_amdgcn_readfirstlane(gwin);
   __syncthreads();  // hs_flag cleared before any wave can poll or raise it
   F2_MARK(1);
   if (!valid || len != XS_BLOCK_DATA) {
     // rejected descriptor or partial block: the fused-v1 order (the other waves idle)
     if (wave == 0) {
       if (valid) {
-        keygen_wave_body<MODE>(key, nn, soff, doff, len, &kl, pw, nullptr, nullptr);
+        keygen_wave_body<MODE>(key, nn, soff, doff, len, &kl, nullptr, nullptr);
       } else if (l == 0u) {
         kl.flags = 1;
         kl.len = 0;
@@ -1953,6 +1955,7 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
 #pragma unroll 1
       for (uint32_t g = 0; g < gn; g++) {
         const uint32_t u = g0 + g;
+        if (!((gwin >> u) & 1u)) continue;  // outside the window: staged for the tag only
         uint32_t ks[16];
         salsa20_block_pre(pre, 64u * u + l, ks);
         F2_MARK(3 + 2 * g);
@@ -2024,7 +2027,7 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
         F2_MARK(3);
       };
       // the descriptor fields this kernel already holds (no second read over PCIe); wave 0's subkey
-      keygen_wave_body<MODE>(key, nn, soff, doff, len, &kl, pw, hs_key[0], &hs_flag[0], z_table);
+      keygen_wave_body<MODE>(key, nn, soff, doff, len, &kl, hs_key[0], &hs_flag[0], z_table, &hs_flag[5]);
     }
     xs_v4i acc[4][2];
     P5 tl;  // wave 0, lane 63: the Poly1305 terms of chunks 4094, 4095
@@ -2101,6 +2104,18 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
             *reinterpret_cast<xs_v4i*>(xacc + (wave - 1u) * 2048u + (uint32_t)(2 * j + mt) * 256u + 4u * l) = acc[j][mt];
       }
     }
+    P5 rexp;  // wave 0: its lane's column exponent r^e, e = 66 - (4n + kg), formed before B2
+    if (wave == 0) {
+      lds_wait_flag(&hs_flag[5]);  // C and D are in kl
+      const uint32_t e = 66u - (4u * n + kg);
+      P5 t1, t2;
+#pragma unroll
+      for (int i = 0; i < 5; i++) {
+        t1.v[i] = kl.full.C[e & 7u][i];
+        t2.v[i] = kl.full.D[e >> 3][i];
+      }
+      rexp = pmul(t2, t1);
+    }
     __syncthreads();  // B2: the other waves' accumulators are in LDS
     F2_MARK(13);
     if (wave == 0) {
@@ -2134,18 +2149,7 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
         }
       }
       const BlockKey* bk = &kl;
-      P5 hs;
-      {
-        const P5 V = column_value(xw);
-        const uint32_t e = 66u - (4u * n + kg);
-        P5 t1, t2;
-#pragma unroll
-        for (int i = 0; i < 5; i++) {
-          t1.v[i] = bk->full.C[e & 7u][i];
-          t2.v[i] = bk->full.D[e >> 3][i];
-        }
-        hs = pmul(V, pmul(t2, t1));
-      }
+      P5 hs = pmul(column_value(xw), rexp);
       if (l == 0u) {
 #pragma unroll
         for (int i = 0; i < 5; i++) hs.v[i] += bk->corr[i];
@@ -2155,12 +2159,7 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
         for (int i = 0; i < 5; i++) hs.v[i] += tl.v[i];
       }
       pnorm(hs);
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-        for (int i = 0; i < 5; i++) hs.v[i] += (uint32_t)__shfl_xor((int)hs.v[i], off, 64);
-        if (off == 2) pnorm(hs);
-      }
+      wave_sum5(hs);
       uint32_t verdict = 1;
       if (l == 0) {
         const P5 hc = pcanon(hs);

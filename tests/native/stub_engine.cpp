@@ -44,6 +44,7 @@ std::vector<int> default_devices() { return {0}; }
 struct xs_engine {
   std::mutex mu;
   uint64_t calls = 0;
+  uint64_t ranged = 0;
 };
 struct xs_pool {
   xs_engine e[2];
@@ -101,6 +102,27 @@ int xs_engine_open(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24]
     }
     ok[j] = orc_secretbox_open(out + j * XS_BLOCK_DATA, in + j * XS_BLOCK_SIZE, blen, n, key) == 0;
     if (!ok[j]) memset(out + j * XS_BLOCK_DATA, 0, blen - XS_BLOCK_HDR);
+  }
+  return XS_OK;
+}
+
+// Ranged open: the bytes outside [range_lo, range_hi) of a verified block are poisoned (0xA5), so a
+// decrypter that serves bytes outside the range it asked for fails the harness's content checks.
+int xs_engine_open_range(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24], uint64_t first_block,
+                         const void* body, uint64_t body_len, void* plain, uint8_t* ok, uint64_t range_lo,
+                         uint64_t range_hi) {
+  const int rc = xs_engine_open(e, key, nonce0, first_block, body, body_len, plain, ok);
+  if (rc != XS_OK) return rc;
+  std::lock_guard<std::mutex> g(e->mu);
+  e->ranged++;
+  uint8_t* out = (uint8_t*)plain;
+  for (uint64_t j = 0; j * XS_BLOCK_SIZE < body_len; j++) {
+    if (!ok[j]) continue;  // a failed block stays zero-filled whole
+    const uint64_t blen = body_len - j * XS_BLOCK_SIZE < XS_BLOCK_SIZE ? body_len - j * XS_BLOCK_SIZE : XS_BLOCK_SIZE;
+    for (uint64_t b = 0; b < blen - XS_BLOCK_HDR; b++) {
+      const uint64_t pos = j * XS_BLOCK_DATA + b;
+      if (pos < range_lo || pos >= range_hi) out[pos] = 0xA5;
+    }
   }
   return XS_OK;
 }
