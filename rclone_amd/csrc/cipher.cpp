@@ -438,6 +438,7 @@ struct rc_encrypter {
   // the other wire buffer.  md5 covers every byte produced once `job` is done; md5_cur is the
   // state before the batch being served (for a consumer that stops inside a batch).
   bool md5_on = false;
+  bool md5_counted = false;  // in g_md5_streams
   bool wsel = false;  // md5_on: the batch being served is in wire2 (else wire)
   PinnedBuf wire2;
   xs::HostMd5 md5, md5_cur;
@@ -449,8 +450,42 @@ static const uint8_t* enc_cur(const rc_encrypter* fh) {
   return fh->in_hdr ? fh->hdr : (fh->md5_on && fh->wsel ? fh->wire2.p : fh->wire.p);
 }
 
+// Per-object hashing (the tee and computeHashWithNonce) hashes batch k on a worker while the stream
+// reads and seals batch k+1.  MD5 is the slowest stage (one chain, ~1 GB/s against several GB/s of
+// reads and seals), so what a stream loses is the time before its chain starts and any gap in it.
+// With the ramp a stream's seals double from one block -- the chain starts after one block's read
+// and seal, not a whole batch's, and each next batch is read and sealed while the previous, half
+// as large, is hashed -- and every batch from one full block up goes to a worker.  The ramp costs
+// more GPU calls and hand-offs, which pay only while each stream has a core to spare for its
+// worker: it is on while the per-object streams hashing now are at most half the process's CPU
+// budget (the reference defaults, --transfers 4 / --checkers 8, on 16 cores), else a stream uses
+// full batches and a 256 KiB inline threshold as before.  RCLONE_AMD_MD5_RAMP=0 turns it off.
+static std::atomic<int> g_md5_streams{0};  // tee encrypters until they finish + hash calls running
+
+static bool md5_ramp_now() {
+  static const bool on = [] {
+    const char* e = getenv("RCLONE_AMD_MD5_RAMP");
+    return !e || atoi(e) != 0;
+  }();
+  static const int cpus = std::max(1, xs::effective_cpus());
+  return on && 2 * g_md5_streams.load(std::memory_order_relaxed) <= cpus;
+}
+
 // Batches below this are hashed on the stream's own thread (a worker hand-off costs ~10 us).
-constexpr int64_t kInlineMd5 = 256 << 10;
+static int64_t inline_md5_below(bool ramping) {
+  static const int64_t env = [] {
+    const char* e = getenv("RCLONE_AMD_MD5_INLINE");
+    return e ? (int64_t)std::max(0, atoi(e)) : (int64_t)-1;
+  }();
+  if (env >= 0) return env;
+  return ramping ? (int64_t)kBlockData : (int64_t)(256 << 10);
+}
+
+static void md5_stream_count(bool& counted, bool on) {
+  if (on == counted) return;
+  counted = on;
+  g_md5_streams.fetch_add(on ? 1 : -1, std::memory_order_relaxed);
+}
 
 // finish (cipher.go:748-758)
 static int64_t enc_finish(rc_encrypter* fh, int32_t err, int32_t* out_err) {
@@ -460,6 +495,7 @@ static int64_t enc_finish(rc_encrypter* fh, int32_t err, int32_t* out_err) {
   }
   fh->finished = true;
   fh->err = err;
+  md5_stream_count(fh->md5_counted, false);
   xs::md5_wait(&fh->job);  // the worker may still be reading a wire buffer
   fh->plain.release();
   fh->wire.release();
@@ -541,6 +577,9 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
     }
     if (nb == 0) return enc_finish(fh, first_err, err);
     fh->grow = grow_batch(fh->c, batch, total, std::chrono::steady_clock::now() - t0);
+    const bool ramp = fh->md5_on && md5_ramp_now();
+    if (ramp && fh->c->growth == 0)  // keep the tee's chain fed: double, no jump to full batches
+      fh->grow = std::min<uint32_t>(2 * batch, fh->c->batch_blocks);
     // with the tee hash on, seal into the wire buffer that is neither served nor being hashed
     const bool into2 = fh->md5_on && !fh->wsel;
     uint8_t* out = into2 ? fh->wire2.p : fh->wire.p;
@@ -560,7 +599,7 @@ extern "C" int64_t rc_encrypter_read(rc_encrypter* fh, uint8_t* p, int64_t n, in
       fh->job.st = &fh->md5;
       fh->job.p = out;
       fh->job.n = (size_t)fh->buf_size;
-      if (fh->buf_size < kInlineMd5) fh->md5.update(out, (size_t)fh->buf_size);
+      if (fh->buf_size < inline_md5_below(ramp)) fh->md5.update(out, (size_t)fh->buf_size);
       else w.submit(&fh->job);
       pc.mark(kEncInline);
     }
@@ -579,6 +618,7 @@ extern "C" int32_t rc_encrypter_set_md5(rc_encrypter* fh, int32_t on) {
   std::lock_guard<std::mutex> g(fh->mu);
   if (!fh->in_hdr || fh->buf_index != 0 || fh->finished) return RC_ERR_INVALID;  // before the first Read only
   fh->md5_on = on != 0;
+  md5_stream_count(fh->md5_counted, fh->md5_on);
   fh->md5 = xs::HostMd5();
   fh->md5_cur = fh->md5;
   if (fh->md5_on) fh->md5.update(fh->hdr, kFileHdr);  // the header is the first "batch" served
@@ -603,6 +643,7 @@ extern "C" int32_t rc_encrypter_md5(rc_encrypter* fh, uint8_t out[16]) {
 
 extern "C" void rc_encrypter_free(rc_encrypter* fh) {
   if (!fh) return;
+  md5_stream_count(fh->md5_counted, false);
   xs::md5_wait(&fh->job);
   delete fh;
 }
@@ -1011,7 +1052,8 @@ extern "C" int32_t rc_hash_batch_with_nonce(rc_cipher* c, uint64_t n, const rc_r
 // computeHashWithNonce (crypt.go:784-806) as an unchanged caller runs it: one object per call, from
 // cryptcheck's --checkers goroutines (cmd/cryptcheck/cryptcheck.go:91-114) or bisync's check.  The
 // object is read in ReadFills of one block, as newEncrypter would, up to hash_batch_blocks() blocks
-// per GPU seal (concurrent callers' seals are group-committed by the engine).  The MD5 of
+// per GPU seal, ramping 1, 2, 4, ... from the first (md5_ramp_now; concurrent callers' seals are
+// group-committed by the engine).  The MD5 of
 // "RCLONE\0\0" || nonce || wire blocks runs on a host core: with a handful of objects in flight a
 // core is ~10x a GPU lane (one dependency chain per stream).  A worker hashes
 // batch k while this thread reads and seals batch k+1 into the other wire buffer.
@@ -1041,7 +1083,11 @@ extern "C" int32_t rc_compute_hash_with_nonce(rc_cipher* c, rc_reader src, const
   int32_t err = RC_NIL;
   PhaseClock pc;
   pc.count(kHashCalls);
-  for (int k = 0;; k ^= 1) {
+  bool counted = false;
+  md5_stream_count(counted, true);
+  bool ramp = md5_ramp_now();
+  uint32_t cur = ramp ? 1u : batch;  // blocks in this seal: 1, 2, 4, ... batch while ramping
+  for (int k = 0;; k ^= 1, ramp = md5_ramp_now(), cur = ramp ? std::min(2 * cur, batch) : batch) {
     if (!plain.ensure((size_t)batch * kBlockData, node) || !wire[k].ensure((size_t)batch * kBlockSize, node)) {
       err = RC_ERR_GPU;
       break;
@@ -1050,7 +1096,7 @@ extern "C" int32_t rc_compute_hash_with_nonce(rc_cipher* c, rc_reader src, const
     uint32_t nb = 0;
     bool end = false, short_read = false;
     int32_t e = RC_NIL;
-    for (; nb < batch; nb++) {
+    for (; nb < cur; nb++) {
       const int64_t got = read_fill(src, plain.p + (int64_t)nb * kBlockData, kBlockData, &e);
       if (got == 0) {  // encrypter.Read: n == 0 -> finish(err); io.Copy ends (EOF = success)
         end = true;
@@ -1077,7 +1123,7 @@ extern "C" int32_t rc_compute_hash_with_nonce(rc_cipher* c, rc_reader src, const
       job.n = (size_t)(total + (int64_t)nb * kBlockHdr);
       // the stream's (probably) last batch: nothing is left to overlap it with, so no hand-off to
       // a scalar worker -- this thread, or an engine lane once the cores are all hashing
-      if ((int64_t)job.n < kInlineMd5) m.update(job.p, job.n);
+      if ((int64_t)job.n < inline_md5_below(ramp)) m.update(job.p, job.n);
       else w.submit(&job, !(end || short_read));
       pc.mark(kHashInline);
     }
@@ -1087,6 +1133,7 @@ extern "C" int32_t rc_compute_hash_with_nonce(rc_cipher* c, rc_reader src, const
     }
   }
   w.wait(&job);
+  md5_stream_count(counted, false);
   // the reference returns hashStr with CheckClose's error: the digest is set whenever the reads
   // succeeded, also when the close then fails
   if (err == RC_NIL) m.final(md5);
