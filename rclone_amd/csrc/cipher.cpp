@@ -357,7 +357,7 @@ extern "C" const char* rc_error_string(int32_t e) {
 // MD5, consumer-side copies are the rest).  Off: one predictable branch per refill.
 namespace {
 enum Phase { kEncRead, kEncSeal, kEncWait, kEncInline, kEncRefills, kHashRead, kHashSeal, kHashWait, kHashInline,
-             kHashCalls, kNPhase };
+             kHashCalls, kHashFinal, kNPhase };
 std::atomic<uint64_t> g_phase[kNPhase];
 bool phases_on() {
   static const bool on = [] {
@@ -365,7 +365,8 @@ bool phases_on() {
     if (!v || atoi(v) == 0) return false;
     atexit([] {
       static const char* names[kNPhase] = {"enc_read", "enc_seal", "enc_md5_wait", "enc_md5_inline", "enc_refills",
-                                           "hash_read", "hash_seal", "hash_md5_wait", "hash_md5_inline", "hash_calls"};
+                                           "hash_read", "hash_seal", "hash_md5_wait", "hash_md5_inline", "hash_calls",
+                                           "hash_final_wait"};
       fprintf(stderr, "{\"rclone_amd_phases\": {");
       for (int i = 0; i < kNPhase; i++) {
         const bool count = i == kEncRefills || i == kHashCalls;
@@ -373,9 +374,12 @@ bool phases_on() {
                 count ? (double)g_phase[i].load() : g_phase[i].load() * 1e-9);
       }
       auto& t = xs::md5_tier_stats();
-      fprintf(stderr, ", \"md5_jobs_worker\": %llu, \"md5_jobs_inline\": %llu, \"md5_jobs_lanes\": %llu}}\n",
+      const double ws = t.worker_ns.load() * 1e-9;
+      fprintf(stderr,
+              ", \"md5_jobs_worker\": %llu, \"md5_jobs_inline\": %llu, \"md5_jobs_lanes\": %llu, "
+              "\"md5_worker_s\": %.4f, \"md5_worker_GB_s\": %.3f}}\n",
               (unsigned long long)t.worker.load(), (unsigned long long)t.inline_.load(),
-              (unsigned long long)t.lanes.load());
+              (unsigned long long)t.lanes.load(), ws, ws > 0 ? t.worker_bytes.load() / ws * 1e-9 : 0.0);
     });
     return true;
   }();
@@ -1133,6 +1137,7 @@ extern "C" int32_t rc_compute_hash_with_nonce(rc_cipher* c, rc_reader src, const
     }
   }
   w.wait(&job);
+  pc.mark(kHashFinal);
   md5_stream_count(counted, false);
   // the reference returns hashStr with CheckClose's error: the digest is set whenever the reads
   // succeeded, also when the close then fails

@@ -18,6 +18,7 @@
 #pragma once
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -47,6 +48,7 @@ struct Md5Job {
 // Where jobs went (cumulative, all nodes): scalar workers, callers' threads, engine lanes.
 struct Md5TierStats {
   std::atomic<uint64_t> worker{0}, inline_{0}, lanes{0};
+  std::atomic<uint64_t> worker_ns{0}, worker_bytes{0};  // scalar workers' hashing time and bytes
 };
 inline Md5TierStats& md5_tier_stats() {
   static Md5TierStats* s = new Md5TierStats();
@@ -72,6 +74,7 @@ class Md5Workers {
         j->owner = this;
         j->busy.store(1, std::memory_order_relaxed);
         q_.push_back(j);
+        qn_.fetch_add(1, std::memory_order_relaxed);
         if (spawn)
           th_.emplace_back([this] {
             pin_thread_to_node(node_);  // the node of the engines whose streams it hashes
@@ -128,13 +131,28 @@ class Md5Workers {
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
       idle_++;
+      if (q_.empty() && spin_ns_ > 0) {  // a stream's next batch usually follows within ~0.1-1 ms
+        lk.unlock();
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned k = 0; qn_.load(std::memory_order_relaxed) == 0; k++) {
+          __builtin_ia32_pause();
+          if ((k & 63u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::nanoseconds(spin_ns_)) break;
+        }
+        lk.lock();
+      }
       cv_.wait(lk, [&] { return !q_.empty(); });
       idle_--;
       Md5Job* j = q_.front();
       q_.pop_front();
+      qn_.fetch_sub(1, std::memory_order_relaxed);
       busy_workers_.fetch_add(1, std::memory_order_relaxed);
       lk.unlock();
+      const auto t0 = std::chrono::steady_clock::now();
       j->st->update(j->p, j->n);
+      md5_tier_stats().worker_ns.fetch_add(
+          (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
+          std::memory_order_relaxed);
+      md5_tier_stats().worker_bytes.fetch_add(j->n, std::memory_order_relaxed);
       lk.lock();
       busy_workers_.fetch_sub(1, std::memory_order_relaxed);
       finish(j);
@@ -208,6 +226,11 @@ class Md5Workers {
   std::deque<Md5Job*> q_, lq_;
   std::vector<std::thread> th_, lth_;
   int idle_ = 0, lane_idle_ = 0, lane_active_ = 0;
+  std::atomic<int> qn_{0};  // q_.size(), readable without mu_ (spinning workers)
+  const int64_t spin_ns_ = [] {
+    const char* v = getenv("XS_MD5_SPIN_US");
+    return v ? (int64_t)atoll(v) * 1000 : (int64_t)0;
+  }();
   std::atomic<int> inline_{0}, busy_workers_{0};
 };
 

@@ -84,10 +84,13 @@ class HostMd5 {
 // (one step's latency is the stream's rate: MD5 is one dependency chain):
 //   F = z ^ (x & (y ^ z)): and, xor;  G = (x & z) + (y & ~z) (disjoint bits): the y & ~z half
 //   joins the early sum, leaving one and;  H = x ^ (y ^ z): one xor;  I = y ^ (x | ~z): or, xor.
-#define XS_F(w, x, y, z, mk) w += (mk); w += (z) ^ ((x) & ((y) ^ (z)))
-#define XS_G(w, x, y, z, mk) w += (mk) + ((y) & ~(z)); w += (x) & (z)
-#define XS_H(w, x, y, z, mk) w += (mk); w += (x) ^ ((y) ^ (z))
-#define XS_I(w, x, y, z, mk) w += (mk); w += (y) ^ ((x) | ~(z))
+// XS_EARLY pins that order: clang otherwise re-associates the sum and puts an add back on the
+// chain (its build ran ~20% below gcc's).
+#define XS_EARLY(w) __asm__("" : "+r"(w))
+#define XS_F(w, x, y, z, mk) w += (mk); XS_EARLY(w); w += (z) ^ ((x) & ((y) ^ (z)))
+#define XS_G(w, x, y, z, mk) w += (mk) + ((y) & ~(z)); XS_EARLY(w); w += (x) & (z)
+#define XS_H(w, x, y, z, mk) w += (mk); XS_EARLY(w); w += (x) ^ ((y) ^ (z))
+#define XS_I(w, x, y, z, mk) w += (mk); XS_EARLY(w); w += (y) ^ ((x) | ~(z))
 #define XS_STEP(f, w, x, y, z, k, t, s) \
   f(w, x, y, z, m[k] + (uint32_t)(t));   \
   w = x + rol(w, s)
@@ -160,6 +163,7 @@ class HostMd5 {
 #undef XS_H
 #undef XS_G
 #undef XS_F
+#undef XS_EARLY
       a0 += a;
       b0 += b;
       c0 += c;
