@@ -74,7 +74,6 @@ class Md5Workers {
         j->owner = this;
         j->busy.store(1, std::memory_order_relaxed);
         q_.push_back(j);
-        qn_.fetch_add(1, std::memory_order_relaxed);
         if (spawn)
           th_.emplace_back([this] {
             pin_thread_to_node(node_);  // the node of the engines whose streams it hashes
@@ -131,20 +130,10 @@ class Md5Workers {
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
       idle_++;
-      if (q_.empty() && spin_ns_ > 0) {  // a stream's next batch usually follows within ~0.1-1 ms
-        lk.unlock();
-        const auto t0 = std::chrono::steady_clock::now();
-        for (unsigned k = 0; qn_.load(std::memory_order_relaxed) == 0; k++) {
-          __builtin_ia32_pause();
-          if ((k & 63u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::nanoseconds(spin_ns_)) break;
-        }
-        lk.lock();
-      }
       cv_.wait(lk, [&] { return !q_.empty(); });
       idle_--;
       Md5Job* j = q_.front();
       q_.pop_front();
-      qn_.fetch_sub(1, std::memory_order_relaxed);
       busy_workers_.fetch_add(1, std::memory_order_relaxed);
       lk.unlock();
       const auto t0 = std::chrono::steady_clock::now();
@@ -226,11 +215,6 @@ class Md5Workers {
   std::deque<Md5Job*> q_, lq_;
   std::vector<std::thread> th_, lth_;
   int idle_ = 0, lane_idle_ = 0, lane_active_ = 0;
-  std::atomic<int> qn_{0};  // q_.size(), readable without mu_ (spinning workers)
-  const int64_t spin_ns_ = [] {
-    const char* v = getenv("XS_MD5_SPIN_US");
-    return v ? (int64_t)atoll(v) * 1000 : (int64_t)0;
-  }();
   std::atomic<int> inline_{0}, busy_workers_{0};
 };
 
