@@ -36,7 +36,6 @@ BLOCK_SIZE = 65552
 ALG_BYTES_SEAL = 65536 + 65552
 ALG_BYTES_OPEN = 65552 + 65536 + 1
 VALU_CYC, SIMDS, CLOCK_HZ = 4, 256 * 4, 2.4e9
-MFMA_HOLD_CYC = 8  # v_mfma_i32_16x16x64_i8: 16 cycles on the matrix pipe, vector issue held for 8
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -66,7 +65,88 @@ def parse():
                     help="file-name mode (SURVEY 8(f) rank 4): encrypt + decrypt this many names per step "
                          "through rc_names_run (0 = the default crypt-block bench)")
     ap.add_argument("--name-paths", action="store_true", help="names mode: 3-segment paths instead of one segment")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch check only: start the ranks, join the process group (gloo, CPU), all-reduce a "
+                         "per-rank counter and print the line with value null; no device work")
     return ap.parse_args()
+
+
+def launch_ranks(args):
+    """`--gpus N` (N > 1) started without a launcher: start N ranks of this same command, one
+    process per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), and exit
+    with the first non-zero rank status (the other ranks are then stopped by PID).  Runs before
+    anything touches the GPU: the children are fresh interpreters, never an exec of this one.
+    Only rank 0 prints the JSON line."""
+    import signal
+    import socket
+    import subprocess
+    n = args.gpus
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            c = p.poll()
+            if c is None:
+                continue
+            pending.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench: rank {procs.index(p)} exited with status {c}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                stop()
+        time.sleep(0.02)
+    return rc
+
+
+def rank_topology(dist, world, dev):
+    """What the job actually ran on: the process group's own world size and each rank's GPU
+    (PCI domain:bus:device, gathered with one small all-reduce).  `distinct_gpus` < ranks means
+    ranks shared a GPU (the gloo rehearsal on a one-GPU box)."""
+    import torch
+    p = torch.cuda.get_device_properties(dev)
+    me = (p.pci_domain_id << 16) | (p.pci_bus_id << 8) | p.pci_device_id
+    if world == 1:
+        ids = [me]
+        seen = 1
+    else:
+        seen = dist.get_world_size()
+        t = torch.zeros(world, dtype=torch.int64, device=dev)
+        t[dist.get_rank()] = me
+        dist.all_reduce(t)
+        ids = [int(x) for x in t.cpu().tolist()]
+    bus = ["%04x:%02x:%02x" % (i >> 16, (i >> 8) & 0xFF, i & 0xFF) for i in ids]
+    return {"ranks_seen": seen, "rank_gpus": bus, "distinct_gpus": len(set(ids))}
+
+
+def run_dry(args, world, rank, dist):
+    """--dry-run: the launch and the collective without any device work (CPU test of N > 1)."""
+    import torch
+    seen = dist.get_world_size() if world > 1 else 1
+    t = torch.tensor([1, rank], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True,
+                          "config": {"ranks_seen": seen, "ranks_reported": int(t[0]), "rank_sum": int(t[1])}}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def cpu_baseline(seconds):
@@ -178,13 +258,11 @@ def issue_bound(valu_insts, ms, clock_hz=None, mfma_insts=None):
     res = {"bound": "valu", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "G wave-instr/s",
            "frac": round(achieved / peak, 4), "valu_wave_insts": valu_insts, "cycles_per_inst": VALU_CYC}
     if mfma_insts is not None:
+        # The MFMAs' own issue cost is left out: SQ_VALU_MFMA_COEXEC_CYCLES shows vector
+        # instructions issuing in about half of the matrix pipe's busy cycles, so no fixed
+        # per-MFMA hold is a bound (round 3's 8-cycle hold model printed fractions above 1).
         res.update({"mfma_wave_insts": mfma_insts, "vector_wave_insts": vector,
                     "counted": "SQ_INSTS_VALU - SQ_INSTS_VALU_MFMA_I8 (MFMAs run on the matrix pipe)"})
-        if clock_hz:
-            # upper model: each MFMA also holds the SIMD's vector issue for 8 of its 16 cycles
-            # (MI355X_MICROARCH.md constants, 'vector-instruction ISSUE cost')
-            cyc = (vector * VALU_CYC + mfma_insts * MFMA_HOLD_CYC) / SIMDS
-            res["frac_at_window_clock_with_mfma_hold"] = round(cyc / (ms * 1e-3 * clock_hz), 4)
     if clock_hz:
         peak_w = SIMDS * clock_hz / VALU_CYC / 1e9
         res.update({"window_clock_ghz": round(clock_hz / 1e9, 4), "peak_at_window_clock": round(peak_w, 1),
@@ -239,7 +317,8 @@ def run_objectset(args, world, rank, dev, dist):
                                    f"TiB) round-robin over {world} rank(s), {args.blocks}-block rounds, seal then "
                                    f"open+verify (BASELINE configs[3])",
                        "object_blocks": args.object_blocks, "round_blocks": args.blocks,
-                       "parallelism": f"{world} rank(s), blocks sharded, counters all-reduced"},
+                       "parallelism": f"{world} rank(s), blocks sharded, counters all-reduced", **args.topo},
+            "build_id": args.build_id,
             "seal_kernel_GiB_s": round(r.n * BLOCK_DATA * args.steps / 2**30 / (sum(seal_ms) * 1e-3), 3),
             "open_kernel_GiB_s": round(r.n * BLOCK_DATA * args.steps / 2**30 / (sum(open_ms) * 1e-3), 3),
             "counters": {"blocks": blocks, "bytes": nbytes, "tag_failures": fails, "roundtrip_mismatch_words": mism,
@@ -388,7 +467,8 @@ def run_mixed(args, world, rank, dev, dist):
                                    f"partial), {nbad} tampered; seal + open+verify as descriptor batches "
                                    f"(BASELINE configs[2])",
                        "objects": len(sizes), "blocks": nb, "tampered_blocks": nbad,
-                       "parallelism": f"{world} rank(s), one object set each, counters all-reduced"},
+                       "parallelism": f"{world} rank(s), one object set each, counters all-reduced", **args.topo},
+            "build_id": args.build_id,
             "seal_GiB_s": round(plain_bytes / 2**30 / (seal_avg * 1e-3), 3),
             "open_GiB_s": round(plain_bytes / 2**30 / (open_avg * 1e-3), 3),
             "roofline": {"bound": "hbm", "kernel": "xs_open", "achieved": round(alg_open / (open_avg * 1e-3) / 1e9, 1),
@@ -514,7 +594,8 @@ def run_names(args, world, rank):
             "data": "synthetic (lowercase names, 8-64 bytes)",
             "config": {"workload": f"{n} {'3-segment paths' if args.name_paths else 'names'} per rank, "
                                    "EncryptFileName then DecryptFileName, base32, standard mode",
-                       "names_per_rank": n, "paths": bool(args.name_paths)},
+                       "names_per_rank": n, "paths": bool(args.name_paths), **args.topo},
+            "build_id": args.build_id,
             "encrypt_s": round(float(np.mean(t_e)), 4), "decrypt_s": round(float(np.mean(t_d)), 4),
             "kernel": {"encrypt_ms": round(ke, 4), "decrypt_ms": round(kd, 4),
                        "segments_per_launch": n * (3 if args.name_paths else 1),
@@ -532,17 +613,32 @@ def run_names(args, world, rank):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+                         f"(--nproc-per-node {args.gpus}) or drop the launcher and let bench.py start the ranks")
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # BENCH_DIST_BACKEND=gloo rehearses the N>1 path on a box with fewer GPUs than ranks (ranks
     # share GPUs round-robin; counters and times go through gloo).  The real run is RCCL, one
     # rank per GPU.
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
-    gpu = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        return run_dry(args, world, rank, dist)
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > 1 and ndev < world:
+        raise SystemExit(f"bench: {world} ranks over RCCL need {world} GPUs, {ndev} visible "
+                         "(BENCH_DIST_BACKEND=gloo rehearses ranks sharing GPUs)")
+    gpu = local % max(ndev, 1) if backend == "gloo" else local
     # the C library's engines (rc_* handles, file names) run on this rank's GPU too
     os.environ.setdefault("RCLONE_AMD_DEVICE", str(gpu))
     if world > 1:
@@ -553,6 +649,12 @@ def main():
             dist.init_process_group(backend)
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
+    from rclone_amd import _lib
+    _lib.lib()  # refuses a library not built from this tree's sources (build id)
+    args.build_id = _lib.build_id()
+    args.topo = rank_topology(dist, world, dev)
+    if args.topo["ranks_seen"] != args.gpus:
+        raise SystemExit(f"bench: process group has {args.topo['ranks_seen']} ranks, --gpus {args.gpus}")
 
     if args.object_blocks:
         return run_objectset(args, world, rank, dev, dist)
@@ -702,7 +804,8 @@ def main():
                                     f"one {world * nb}-block object)") +
                                    ", seal then open+verify (BASELINE configs[1]+[2] shape)",
                        "blocks_per_gpu": nb, "block_bytes": BLOCK_DATA,
-                       "parallelism": f"{world} rank(s), blocks sharded, no data-path collective"},
+                       "parallelism": f"{world} rank(s), blocks sharded, no data-path collective", **args.topo},
+            "build_id": args.build_id,
             "seal_GiB_s": round(nb * BLOCK_DATA / 2**30 / (seal_avg * 1e-3), 3),
             "open_GiB_s": round(nb * BLOCK_DATA / 2**30 / (open_avg * 1e-3), 3),
             "roofline": {"bound": "hbm", "kernel": "xs_seal",

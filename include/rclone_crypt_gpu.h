@@ -70,6 +70,9 @@ typedef struct xs_md5_desc {
 } xs_md5_desc;  /* 64 bytes */
 
 const char *xs_version(void);
+/* sha256 (hex) of the sources and build flags the library was compiled from
+   (rclone_amd/build.py build_sources_sha256); "unstamped" for a build outside it. */
+const char *xs_build_id(void);
 /* Last error message of the calling thread ("" if none). */
 const char *xs_last_error(void);
 /* Number of HIP devices (0 when none; never fails). */
@@ -230,6 +233,7 @@ void xs_host_free(void *p);
  * RCLONE_AMD_SYSFS_ROOT (default /sys); RCLONE_AMD_NUMA=0 turns placement off. */
 int xs_device_numa_node(int device);          /* NUMA node of a HIP device's PCI function, or -1 */
 int xs_engine_numa_node(const xs_engine *e);  /* the node the engine's host resources use, or -1 */
+int xs_engine_device(const xs_engine *e);     /* the HIP device the engine runs on, or -1 */
 int xs_pci_numa_node(const char *pci_bus_id); /* <root>/bus/pci/devices/<id>/numa_node, or -1 */
 /* CPUs of a node (<root>/devices/system/node/node<N>/cpulist): writes up to cap, returns the count
  * (0 when unknown). */

@@ -44,6 +44,7 @@ OPEN_FN = ctypes.CFUNCTYPE(i32, vp, i64, i64, ctypes.POINTER(RcReader))
 # (name, restype, argtypes)
 _SIGS = [
     ("xs_version", ctypes.c_char_p, []),
+    ("xs_build_id", ctypes.c_char_p, []),
     ("xs_last_error", ctypes.c_char_p, []),
     ("xs_device_count", ctypes.c_int, []),
     ("xs_workspace_bytes", ctypes.c_size_t, [u64]),
@@ -82,6 +83,7 @@ _SIGS = [
     ("xs_host_alloc_node", vp, [ctypes.c_size_t, ctypes.c_int]),
     ("xs_device_numa_node", ctypes.c_int, [ctypes.c_int]),
     ("xs_engine_numa_node", ctypes.c_int, [vp]),
+    ("xs_engine_device", ctypes.c_int, [vp]),
     ("xs_pci_numa_node", ctypes.c_int, [ctypes.c_char_p]),
     ("xs_numa_node_cpus", ctypes.c_int, [ctypes.c_int, vp, ctypes.c_int]),
     ("xs_parse_device_list", ctypes.c_int, [ctypes.c_char_p, vp, ctypes.c_int]),
@@ -141,24 +143,45 @@ _SIGS = [
 SYMBOLS = [s[0] for s in _SIGS]
 
 
+class StaleLibraryError(RuntimeError):
+    """The library on disk was not built from this tree's sources (build id mismatch)."""
+
+
 def lib():
-    """Load (building if stale) the native library; raises if it cannot be built/loaded."""
+    """Load the native library built from this tree's sources.  A library whose embedded build id
+    differs from the tree's (rclone_amd/build.py build_sources_sha256) is rebuilt, or refused
+    with StaleLibraryError when RCLONE_AMD_REBUILD=0 or no hipcc is present; a library missing
+    any declared entry point is refused too.  Never a fallback."""
     global _lib
     if _lib is None:
         path = _build.LIB
-        if _build.needs_build():
+        want = _build.build_sources_sha256()
+        have = _build.library_build_id(path)
+        if have != want:
+            if os.environ.get("RCLONE_AMD_REBUILD", "1") == "0" or not os.path.exists(_build.HIPCC):
+                raise StaleLibraryError(
+                    f"{path}: built from sources {have or 'unknown/missing'}, this tree is {want} "
+                    "(rebuild: python -m rclone_amd.build)")
             _build.build()
         if not os.path.exists(path):
             raise RuntimeError(f"rclone_amd native library missing: {path}")
         L = ctypes.CDLL(path)
+        missing = [name for name, _, _ in _SIGS if not hasattr(L, name)]
+        if missing:
+            raise StaleLibraryError(f"{path} lacks entry points {missing}")
         for name, res, args in _SIGS:
-            if not hasattr(L, name):
-                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        got = L.xs_build_id().decode()
+        if got != want:
+            raise StaleLibraryError(f"{path}: loaded library reports build {got}, this tree is {want}")
         _lib = L
     return _lib
+
+
+def build_id():
+    return lib().xs_build_id().decode()
 
 
 def last_error():

@@ -3,19 +3,32 @@
 The .so holds the HIP kernels (csrc/xs_kernels.hip), the device C ABI (csrc/xs_api.cpp) and
 the host mirror of backend/crypt/cipher.go (csrc/cipher.cpp, csrc/scrypt.cpp).  It is
 git-ignored but travels to the GPU box with the repo snapshot.
+
+Provenance: every build embeds `build_sources_sha256()` -- the sha256 of every file under
+csrc/, the public header and the compile command -- as the library's build id
+(`xs_build_id()`, and a tagged string the loader reads from the file without loading it).
+`needs_build()` compares that id with the tree's, not file times, so a library built from other
+sources is never taken for this tree's (rclone_amd/_lib.py rebuilds or refuses it).
 """
+import fcntl
+import hashlib
 import os
+import re
 import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "librclone_crypt.so")
+HEADER = os.path.join(ROOT, "include", "rclone_crypt_gpu.h")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RCLONE_AMD_ARCH", "gfx950")
 
 SOURCES = ["xs_kernels.hip", "xs_md5.hip", "xs_eme.hip", "xs_probe.hip", "xs_api.cpp", "xs_topo.cpp", "cipher.cpp", "names.cpp",
            "names_gpu.cpp", "scrypt.cpp"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-result"]
+BUILD_ID_TAG = b"xs-build-id:"
 
 
 # what the crypt kernels (xs_seal / xs_open / keygen) are compiled from: PMC counters committed under
@@ -25,8 +38,7 @@ KERNEL_SOURCES = ["rclone_amd/csrc/xs_kernels.hip", "rclone_amd/csrc/xs_salsa_la
 
 
 def kernel_sources_sha256(root=None):
-    import hashlib
-    root = root or os.path.dirname(HERE)
+    root = root or ROOT
     h = hashlib.sha256()
     for rel in KERNEL_SOURCES:
         p = os.path.join(root, rel)
@@ -41,26 +53,77 @@ def sources():
     return [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
 
 
+def build_inputs():
+    """Every file the library is compiled from: all of csrc/ (sources and headers) + the C header."""
+    files = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)
+                   if f.endswith((".hip", ".cpp", ".h")))
+    return files + [HEADER]
+
+
+def build_sources_sha256():
+    h = hashlib.sha256()
+    h.update(" ".join([ARCH] + FLAGS + SOURCES).encode() + b"\0")
+    for p in build_inputs():
+        h.update(os.path.relpath(p, ROOT).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def library_build_id(path=LIB):
+    """The build id embedded in a built library file (None if absent or unstamped)."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    m = re.search(re.escape(BUILD_ID_TAG) + rb"([0-9a-f]{64})\0", data)
+    return m.group(1).decode() if m else None
+
+
 def needs_build():
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    deps = sources() + [os.path.join(CSRC, h) for h in ("xs_internal.h", "xs_aes.h", "rc_internal.h", "xs_host_md5.h", "md5_workers.h", "md5_x16.h", "xs_topo.h")] + [
-                        os.path.join(os.path.dirname(HERE), "include", "rclone_crypt_gpu.h")]
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    return library_build_id(LIB) != build_sources_sha256()
 
 
 def build(force=False, verbose=False):
-    if not force and not needs_build():
-        return LIB
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-result", "-o", LIB] + sources() + ["-lpthread"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
+    """Compile into a temporary file and rename it over LIB, under a lock: ranks of one job that
+    find the library stale at the same time build it once, and no process ever maps a
+    half-written file."""
+    with open(LIB + ".lock", "a") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and not needs_build():
+            return LIB
+        bid = build_sources_sha256()
+        tmp = f"{LIB}.tmp{os.getpid()}"
+        # one object per source, compiled in parallel (xs_kernels.hip alone is most of the time),
+        # then one link
+        import tempfile
+        from concurrent.futures import ThreadPoolExecutor
+        with tempfile.TemporaryDirectory(prefix="rclone_amd_build_") as od:
+            def compile_one(src):
+                obj = os.path.join(od, os.path.basename(src) + ".o")
+                cmd = ([HIPCC, f"--offload-arch={ARCH}"] + [f for f in FLAGS if f != "-shared"] +
+                       [f'-DXS_BUILD_ID="{bid}"', "-c", "-o", obj, src])
+                if verbose:
+                    print(" ".join(cmd), file=sys.stderr)
+                subprocess.check_call(cmd)
+                return obj
+            jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
+            with ThreadPoolExecutor(jobs) as ex:
+                objs = list(ex.map(compile_one, sources()))
+            cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lpthread"]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            try:
+                subprocess.check_call(cmd)
+                os.replace(tmp, LIB)
+            finally:
+                if os.path.exists(tmp):
+                    os.unlink(tmp)
     return LIB
 
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
-    print(LIB)
+    print(LIB, build_sources_sha256())

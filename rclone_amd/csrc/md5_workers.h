@@ -16,10 +16,16 @@
 // A stream submits its jobs one at a time (it waits for job k before submitting job k+1), so its
 // bytes are hashed in order whichever tier takes each job.
 #pragma once
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <climits>
 #include <condition_variable>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -38,7 +44,7 @@ struct Md5Job {
   HostMd5* st = nullptr;
   const uint8_t* p = nullptr;
   size_t n = 0;
-  std::atomic<int> busy{0};  // 1 from submit until the bytes are hashed
+  std::atomic<int> busy{0};  // 1 from submit until the bytes are hashed (2: a waiter sleeps on it)
   const Md5Workers* owner = nullptr;
   // multi-buffer engine: the whole blocks left after HostMd5::begin_blocks
   const uint8_t* blk = nullptr;
@@ -110,20 +116,31 @@ class Md5Workers {
     md5_tier_stats().lanes++;
   }
 
+  // Each job has its own wake-up: busy is 1 while hashing, 2 once a waiter sleeps on it (a
+  // private futex on the job's own word), so finishing a job wakes only that job's waiter and
+  // costs no syscall when nobody sleeps -- never a broadcast to every stream's waiter.
   void wait(Md5Job* j) const {
     if (!j->busy.load(std::memory_order_acquire)) return;
     for (int k = 0; k < 64; k++) {  // a job hashes ~1 MiB (~1 ms): spin only briefly
       if (!j->busy.load(std::memory_order_acquire)) return;
       std::this_thread::yield();
     }
-    std::unique_lock<std::mutex> lk(mu_);
-    done_.wait(lk, [&] { return !j->busy.load(std::memory_order_acquire); });
+    for (;;) {
+      int v = j->busy.load(std::memory_order_acquire);
+      if (v == 0) return;
+      if (v == 1 && !j->busy.compare_exchange_strong(v, 2, std::memory_order_acq_rel)) {
+        if (v == 0) return;
+      }
+      syscall(SYS_futex, reinterpret_cast<int*>(&j->busy), FUTEX_WAIT_PRIVATE, 2, nullptr, nullptr, 0);
+    }
   }
 
  private:
-  void finish(Md5Job* j) {  // under mu_: a waiter checks busy under mu_ too, so no lost wake-up
-    j->busy.store(0, std::memory_order_release);
-    done_.notify_all();
+  static void finish(Md5Job* j) {
+    // the private-futex wake only hashes the address: safe even if the waiter has already seen 0
+    // and released the job
+    if (j->busy.exchange(0, std::memory_order_acq_rel) == 2)
+      syscall(SYS_futex, reinterpret_cast<int*>(&j->busy), FUTEX_WAKE_PRIVATE, INT32_MAX, nullptr, nullptr, 0);
   }
 
   void run() {
@@ -211,7 +228,7 @@ class Md5Workers {
   const bool lanes_on_;
   const int lane_threads_max_;
   mutable std::mutex mu_;
-  mutable std::condition_variable cv_, lcv_, done_;
+  mutable std::condition_variable cv_, lcv_;
   std::deque<Md5Job*> q_, lq_;
   std::vector<std::thread> th_, lth_;
   int idle_ = 0, lane_idle_ = 0, lane_active_ = 0;

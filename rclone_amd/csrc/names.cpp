@@ -681,8 +681,9 @@ constexpr size_t kChunkNames = 8192;
 constexpr unsigned kHostThreads = 16;
 
 // A batch's host stages call parallel_for three or four times; spawning 16 threads each time
-// costs milliseconds per call.  The helpers stay parked between calls (never destroyed).  One
-// batch uses them at a time; a concurrent batch spawns its own threads as before.
+// costs milliseconds per call.  One process-wide set of helpers stays parked between calls (never
+// destroyed) and serves one parallel_for at a time, whichever batch or stage it belongs to; a
+// parallel_for that finds it busy (another batch's stage in flight) spawns its own threads.
 class NamePool {
  public:
   explicit NamePool(unsigned helpers) {
@@ -742,16 +743,21 @@ unsigned name_threads() {
   return nt;
 }
 
-template <class F>
-void parallel_for(size_t n, F f) {
+// the one helper pool of the process (a template-local static would give every call site's
+// lambda type a pool of its own)
+NamePool& name_pool() {
+  static NamePool* pool = new NamePool(name_threads() - 1);
+  return *pool;
+}
+
+void parallel_for_fn(size_t n, const std::function<void(size_t)>& f) {
   const unsigned nt = std::max(1u, std::min(name_threads(), (unsigned)n));
   if (nt <= 1) {
     for (size_t i = 0; i < n; i++) f(i);
     return;
   }
-  static NamePool* pool = new NamePool(name_threads() - 1);
-  const std::function<void(size_t)> fn = f;
-  if (pool->helpers() + 1 >= nt && pool->try_run(n, fn)) return;
+  NamePool& pool = name_pool();
+  if (pool.helpers() + 1 >= nt && pool.try_run(n, f)) return;
   std::atomic<size_t> next{0};
   std::vector<std::thread> th;
   for (unsigned t = 0; t < nt; t++)
@@ -759,6 +765,11 @@ void parallel_for(size_t n, F f) {
       for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
     });
   for (auto& t : th) t.join();
+}
+
+template <class F>
+void parallel_for(size_t n, F f) {
+  parallel_for_fn(n, std::function<void(size_t)>(f));
 }
 
 // All parts' segments in one pinned buffer -> one H2D, one EME launch (in place), one D2H

@@ -113,6 +113,14 @@ extern "C" {
 
 const char* xs_version(void) { return "rclone_amd crypt 0.1 (gfx950)"; }
 
+// sha256 of the sources and build flags this library was compiled from (rclone_amd/build.py
+// passes it in); the tagged copy lets the loader read it from the file without loading it
+#ifndef XS_BUILD_ID
+#define XS_BUILD_ID "unstamped"
+#endif
+__attribute__((used)) static const char kBuildIdTag[] = "xs-build-id:" XS_BUILD_ID;
+const char* xs_build_id(void) { return kBuildIdTag + 12; }
+
 const char* xs_last_error(void) { return g_err.c_str(); }
 
 int xs_device_count(void) {
@@ -608,6 +616,7 @@ extern "C" void xs_engine_stats(xs_engine* e, uint64_t out[3]) {
 extern "C" void xs_engine_destroy(xs_engine* e) { engine_free(e); }
 
 extern "C" int xs_engine_numa_node(const xs_engine* e) { return e ? e->numa : -1; }
+extern "C" int xs_engine_device(const xs_engine* e) { return e ? e->device : -1; }
 
 static int engine_sync(xs_engine* e) {
   int rc = XS_OK;

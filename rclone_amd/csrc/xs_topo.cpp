@@ -109,25 +109,76 @@ int parse_device_list(const char* s, std::vector<int>* out) {
   return (int)out->size();
 }
 
-// CPUs this process can use: its affinity mask, capped by the cgroup CPU quota (v2 cpu.max or v1
-// cpu.cfs_quota_us / cpu.cfs_period_us under the sysfs root); RCLONE_AMD_CPUS overrides.  A GPU
-// box share of 16 cores on a 256-CPU machine is 16, not 256.
+// The process's CPU affinity as it was when the library was loaded (the loading thread's mask:
+// what the operator gave the process with taskset / numactl / the container).  Library threads
+// are pinned inside it, and effective_cpus() counts it, whichever thread asks later -- a thread
+// the library has already pinned to one node must not shrink either.
+static cpu_set_t g_process_cpus;
+static bool g_process_cpus_ok = false;
+
+void capture_process_affinity() {
+  CPU_ZERO(&g_process_cpus);
+  g_process_cpus_ok = sched_getaffinity(0, sizeof g_process_cpus, &g_process_cpus) == 0 && CPU_COUNT(&g_process_cpus) > 0;
+}
+
+[[maybe_unused]] static const bool g_captured_at_load = (capture_process_affinity(), true);
+
+// cgroup v2: the quota that binds this process is the smallest cpu.max on the path from its own
+// group (/proc/self/cgroup "0::/a/b") up to the mount root, so a nested group (a systemd slice
+// with CPUQuota, no cgroup namespace) is honoured as well as a container's root-level file.
+static double cgroup_v2_quota(const std::string& root) {
+  double quota = -1;
+  auto consider = [&](const std::string& dir) {
+    std::string v;
+    if (!read_line(dir + "/cpu.max", &v)) return false;  // "max 100000" or "1600000 100000"
+    long long q = 0, per = 0;
+    if (sscanf(v.c_str(), "%lld %lld", &q, &per) == 2 && q > 0 && per > 0) {
+      const double f = (double)q / (double)per;
+      if (quota < 0 || f < quota) quota = f;
+    }
+    return true;
+  };
+  const char* proc = getenv("RCLONE_AMD_PROC_ROOT");
+  std::string self;
+  FILE* f = fopen(((proc && *proc ? std::string(proc) : std::string("/proc")) + "/self/cgroup").c_str(), "r");
+  if (f) {
+    char buf[4096];
+    while (fgets(buf, sizeof buf, f)) {
+      if (strncmp(buf, "0::", 3) == 0) {
+        self.assign(buf + 3);
+        while (!self.empty() && isspace((unsigned char)self.back())) self.pop_back();
+        break;
+      }
+    }
+    fclose(f);
+  }
+  const std::string base = root + "/fs/cgroup";
+  // walk /a/b -> /a -> "" (the mount root); a path that does not resolve under this mount (a
+  // cgroup namespace shows "/") simply finds no files below the root
+  while (!self.empty() && self != "/" && self.find("..") == std::string::npos) {
+    consider(base + self);
+    const size_t cut = self.find_last_of('/');
+    if (cut == std::string::npos) break;
+    self.resize(cut);
+  }
+  if (!consider(base) && quota < 0) return -2;  // no v2 file at the root either: try v1
+  return quota;
+}
+
+// CPUs this process can use: its affinity mask at load, capped by the cgroup CPU quota (v2
+// cpu.max along the process's own group path, or v1 cpu.cfs_quota_us / cpu.cfs_period_us under
+// the sysfs root); RCLONE_AMD_CPUS overrides.  A GPU box share of 16 cores on a 256-CPU machine
+// is 16, not 256.
 int effective_cpus() {
   if (const char* e = getenv("RCLONE_AMD_CPUS")) {
     const int v = atoi(e);
     if (v > 0) return v;
   }
-  int n = (int)std::thread::hardware_concurrency();
-  cpu_set_t set;
-  CPU_ZERO(&set);
-  if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
-  double quota = -1;
-  std::string v;
+  int n = g_process_cpus_ok ? CPU_COUNT(&g_process_cpus) : (int)std::thread::hardware_concurrency();
   const std::string root = sysfs_root();
-  if (read_line(root + "/fs/cgroup/cpu.max", &v)) {  // "max 100000" or "1600000 100000"
-    long long q = 0, per = 0;
-    if (sscanf(v.c_str(), "%lld %lld", &q, &per) == 2 && q > 0 && per > 0) quota = (double)q / (double)per;
-  } else {
+  double quota = cgroup_v2_quota(root);
+  if (quota == -2) {
+    quota = -1;
     std::string a, b;
     if (read_line(root + "/fs/cgroup/cpu/cpu.cfs_quota_us", &a) && read_line(root + "/fs/cgroup/cpu/cpu.cfs_period_us", &b)) {
       const long long q = atoll(a.c_str()), per = atoll(b.c_str());
@@ -138,8 +189,10 @@ int effective_cpus() {
   return std::max(1, n);
 }
 
-// Pin the calling thread to the CPUs of `node` (no-op when the node or its CPU list is unknown, or
-// RCLONE_AMD_NUMA=0).  Only threads this library starts are pinned -- never a caller's thread.
+// Pin the calling thread to the CPUs of `node` that the process may use (the node's CPU list
+// intersected with the process affinity captured at load).  No-op when the node or its CPU list
+// is unknown, the intersection is empty, or RCLONE_AMD_NUMA=0.  Only threads this library starts
+// are pinned -- never a caller's thread.
 void pin_thread_to_node(int node) {
   if (!numa_enabled()) return;
   std::vector<int> cpus;
@@ -147,7 +200,8 @@ void pin_thread_to_node(int node) {
   cpu_set_t set;
   CPU_ZERO(&set);
   for (int c : cpus)
-    if (c < CPU_SETSIZE) CPU_SET(c, &set);
+    if (c < CPU_SETSIZE && (!g_process_cpus_ok || CPU_ISSET(c, &g_process_cpus))) CPU_SET(c, &set);
+  if (CPU_COUNT(&set) == 0) return;
   (void)sched_setaffinity(0, sizeof set, &set);
 }
 

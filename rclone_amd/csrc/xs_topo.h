@@ -11,7 +11,8 @@ bool node_cpus(int node, std::vector<int>* cpus);           // false when unknow
 int parse_device_list(const char* s, std::vector<int>* out);
 bool numa_enabled();                                        // RCLONE_AMD_NUMA (default 1)
 int effective_cpus();  // affinity, capped by the cgroup CPU quota (RCLONE_AMD_CPUS overrides)
-void pin_thread_to_node(int node);                          // library-started threads only
+void pin_thread_to_node(int node);  // library-started threads only, inside the process's mask
+void capture_process_affinity();    // re-read the process mask (done at load; tests)
 class ScopedMemPolicy {  // preferred-node policy of the calling thread while in scope
  public:
   explicit ScopedMemPolicy(int node);

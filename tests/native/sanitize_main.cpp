@@ -718,6 +718,41 @@ static void test_topology() {
   });
   t.join();
   CHECK(on_cpu0, "thread pinned to the node's CPUs");
+  // a process started under a narrowed mask (taskset / numactl --physcpubind): library threads
+  // stay inside it -- the node's CPUs intersected with the mask, or left alone when disjoint
+  cpu_set_t full;
+  CPU_ZERO(&full);
+  sched_getaffinity(0, sizeof full, &full);
+  if (CPU_ISSET(0, &full) && CPU_ISSET(1, &full) && CPU_ISSET(2, &full)) {
+    put_file(r + "/devices/system/node/node3/cpulist", "0-1\n");
+    cpu_set_t narrow;
+    CPU_ZERO(&narrow);
+    CPU_SET(1, &narrow);
+    CPU_SET(2, &narrow);
+    sched_setaffinity(0, sizeof narrow, &narrow);
+    xs::capture_process_affinity();
+    int inter_ok = 0, disjoint_ok = 0;
+    std::thread t2([&] {
+      xs::pin_thread_to_node(3);  // node {0,1} & mask {1,2} = {1}
+      cpu_set_t s;
+      CPU_ZERO(&s);
+      if (sched_getaffinity(0, sizeof s, &s) == 0) inter_ok = CPU_COUNT(&s) == 1 && CPU_ISSET(1, &s);
+    });
+    t2.join();
+    std::thread t3([&] {
+      xs::pin_thread_to_node(1);  // node {0} & mask {1,2} = {}: unchanged
+      cpu_set_t s;
+      CPU_ZERO(&s);
+      if (sched_getaffinity(0, sizeof s, &s) == 0) disjoint_ok = CPU_EQUAL(&s, &narrow);
+    });
+    t3.join();
+    const int counted = xs::effective_cpus();
+    sched_setaffinity(0, sizeof full, &full);
+    xs::capture_process_affinity();
+    CHECK(inter_ok, "pinning intersects the node with the process mask");
+    CHECK(disjoint_ok, "no pinning outside the process mask when the node is disjoint from it");
+    CHECK(counted == 2 || getenv("RCLONE_AMD_CPUS"), "effective_cpus counts the process mask (%d)", counted);
+  }
   int mode_before = -1, mode_in = -1, mode_after = -1;
   unsigned long mask[16] = {0};
   syscall(SYS_get_mempolicy, &mode_before, mask, 1024ul, nullptr, 0ul);

@@ -79,3 +79,42 @@ def test_owned_blocks_partition():
         assert sorted(seen.tolist()) == list(range(1001))
     with pytest.raises(ValueError):
         shard.owned_blocks(10, 2, 2)
+
+
+def _bench(args, env_extra=None, timeout=180):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], capture_output=True, text=True,
+                       env=env, timeout=timeout, cwd=root)
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, lines
+
+
+def test_bench_starts_its_own_ranks():
+    """`bench.py --gpus 2` with no launcher starts two ranks itself; they join one process group
+    and only rank 0 prints the line, with the world size the group reports."""
+    r, lines = _bench(["--gpus", "2", "--dry-run", "--steps", "3"], {"BENCH_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout
+    res = lines[0]
+    assert res["n_gpus"] == 2 and res["dry_run"] is True
+    assert res["config"] == {"ranks_seen": 2, "ranks_reported": 2, "rank_sum": 1}
+
+
+def test_bench_refuses_gpus_world_mismatch():
+    r, lines = _bench(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "1"})
+    assert r.returncode != 0 and not lines
+    assert "--gpus 2 but WORLD_SIZE=1" in r.stderr
+
+
+def test_bench_rank_failure_fails_the_job():
+    """A rank that cannot run (no GPU here: RCCL ranks need one device each) ends the job with a
+    non-zero status and no result line."""
+    r, lines = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+    assert r.returncode != 0 and not lines
+    assert "need 2 GPUs" in r.stderr or "exited with status" in r.stderr

@@ -10,9 +10,11 @@ corrupted object flagged), every sampled stored object -- the edge files, ~64 sp
 tree, the largest -- is recomputed here from its plaintext seed and stored nonce with the CPU
 oracle: SHA-256 of the whole crypt file and the MD5 crypt.put teed off the ciphertext.
 
-Size: RCLONE_AMD_E2E_GIB (default 16 GiB), capped to what the host can hold -- the tree in
-/dev/shm plus the remote's pinned arena plus 4 x 4 GiB staging -- and printed.  The full
-100 GiB needs ~216 GiB of host memory.
+Size: BASELINE configs[4]'s stated 100 GiB (RCLONE_AMD_E2E_GIB overrides).  It needs ~216 GiB
+of host memory -- the tree in /dev/shm plus the remote's pinned arena plus 4 x 4 GiB staging
+ -- which the GPU box's per-command budget holds.  A host that cannot hold the
+requested size FAILS the test rather than running a smaller one, unless
+RCLONE_AMD_E2E_ALLOW_CAP=1 (then the size is capped and the cap is in the result).
 """
 import hashlib
 import json
@@ -45,13 +47,18 @@ def _mem_available_gib():
 
 
 def _size_gib():
-    want = float(os.environ.get("RCLONE_AMD_E2E_GIB", "16"))
+    want = float(os.environ.get("RCLONE_AMD_E2E_GIB", "100"))
     shm = shutil.disk_usage("/dev/shm").free / 2**30 if os.path.isdir("/dev/shm") else 0.0
     # tree (page cache or shm) + arena + staging (4 lanes x 4 GiB) + slack, within the per-command
     # host memory budget of the GPU box (RCLONE_AMD_E2E_MEM_GIB, default 240 GiB)
     budget = min(_mem_available_gib(), float(os.environ.get("RCLONE_AMD_E2E_MEM_GIB", "240")))
     fits_mem = (budget - 16 - 8) / 2.1
-    return max(1.0, min(want, fits_mem, shm - 4 if shm else want)), shm
+    fits = min(fits_mem, shm - 4 if shm else want)
+    if fits < want and os.environ.get("RCLONE_AMD_E2E_ALLOW_CAP") != "1":
+        pytest.fail(f"configs[4] asks {want:.0f} GiB; this host holds {fits:.1f} GiB (MemAvailable "
+                    f"{_mem_available_gib():.0f} GiB, /dev/shm free {shm:.0f} GiB); set RCLONE_AMD_E2E_GIB "
+                    "or RCLONE_AMD_E2E_ALLOW_CAP=1 to run smaller")
+    return max(1.0, min(want, fits)), shm
 
 
 # the two shapes: batched calls (a changed caller: whole-tree groups through xs_engine_put_batch /
@@ -76,16 +83,20 @@ def test_sync_cryptcheck_oracle_anchored(tmp_path, shape):
     anchor = str(tmp_path / "anchor.jsonl")
     print(f"configs[4] e2e ({shape}) at {gib:.1f} GiB (tree in {base}, MemAvailable {_mem_available_gib():.0f} GiB)")
     try:
+        # the harness's phase lines go to stderr as they happen (a long run shows progress)
         r = subprocess.run([exe, "--gib", "%.3f" % gib, "--dir", tree, "--anchor", anchor] + SHAPES[shape],
-                           capture_output=True, text=True, timeout=800)
+                           stdout=subprocess.PIPE, text=True, timeout=800)
     finally:
         shutil.rmtree(tree, ignore_errors=True)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, r.stdout[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     print(json.dumps(res))
-    assert res["ok"] and res["put_hash_mismatches"] == 0 and res["cryptcheck_differences"] == 0
-    assert res["corruption_flagged"] == 1 and res["verify_failures"] == 0 and res["name_mismatches"] == 0
-    assert res["gib"] >= min(gib, 16.0) * 0.99
+    where = f"configs[4] {shape} at {res.get('gib')} GiB"
+    assert res["ok"] and res["put_hash_mismatches"] == 0 and res["cryptcheck_differences"] == 0, where
+    assert res["corruption_flagged"] == 1 and res["verify_failures"] == 0 and res["name_mismatches"] == 0, where
+    assert res["gib"] >= gib * 0.999, f"ran {res['gib']} GiB of the {gib:.1f} GiB asked"
+    # the size is part of every assertion message below, so a -q run still names it
+    print(f"configs[4] {shape}: {res['gib']} GiB, sync {res['sync_GiB_s']} GiB/s, cryptcheck {res['cryptcheck_GiB_s']} GiB/s")
     if shape == "stream":
         assert res["mode"] == "stream" and res["tee"] == "encrypter" and res["check_mode"] == "stream"
         assert res["transfers"] == 4 and res["checkers"] == 8
@@ -98,5 +109,5 @@ def test_sync_cryptcheck_oracle_anchored(tmp_path, shape):
     for row in rows:
         plain = splitmix64_bytes(row["seed"], row["size"])
         ct = orc.encrypt_file(plain, bytes.fromhex(row["nonce"]), key)
-        assert hashlib.sha256(ct).hexdigest() == row["sha256"], row
-        assert hashlib.md5(ct).hexdigest() == row["tee_md5"], row
+        assert hashlib.sha256(ct).hexdigest() == row["sha256"], (where, row)
+        assert hashlib.md5(ct).hexdigest() == row["tee_md5"], (where, row)

@@ -35,6 +35,58 @@ def test_version_and_devices():
     assert lib.xs_device_count() >= 0
 
 
+def test_build_id_ties_library_to_tree():
+    from rclone_amd import build
+    want = build.build_sources_sha256()
+    assert _lib.build_id() == want == build.library_build_id()
+    assert not build.needs_build()
+
+
+_STALE_PROBE = r"""
+import sys
+sys.path.insert(0, {root!r})
+from rclone_amd import _lib, build
+build.LIB = {path!r}
+try:
+    _lib.lib()
+except _lib.StaleLibraryError as e:
+    print("REFUSED", e)
+else:
+    print("LOADED")
+"""
+
+
+def _probe(tmp_path, data, extra_env=None, patch_check=False):
+    import subprocess
+    import sys
+    p = tmp_path / "librclone_crypt.so"
+    p.write_bytes(data)
+    code = _STALE_PROBE.format(root=ROOT, path=str(p))
+    if patch_check:  # the file check passes: only the loaded library's own xs_build_id() can refuse
+        code = code.replace("build.LIB =", "build.library_build_id = lambda path=None: build.build_sources_sha256()\nbuild.LIB =")
+    env = dict(os.environ, RCLONE_AMD_REBUILD="0", **(extra_env or {}))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return r.stdout
+
+
+def test_stale_library_is_refused(tmp_path):
+    """A library whose embedded build id is not this tree's (built from other sources) is
+    refused, both by the file check before loading and by the loaded library's xs_build_id()."""
+    from rclone_amd import build
+    data = open(build.LIB, "rb").read()
+    want = build.build_sources_sha256().encode()
+    i = data.index(build.BUILD_ID_TAG + want)
+    stale = bytearray(data)
+    j = i + len(build.BUILD_ID_TAG)
+    stale[j:j + 8] = b"00000000" if want[:8] != b"00000000" else b"11111111"
+    assert "LOADED" in _probe(tmp_path, bytes(data))
+    out = _probe(tmp_path, bytes(stale))
+    assert "REFUSED" in out and "built from sources" in out
+    out = _probe(tmp_path, bytes(stale), patch_check=True)
+    assert "REFUSED" in out and "loaded library reports build" in out
+
+
 def test_encrypted_decrypted_size(ref_kat):
     for n, e in ref_kat["encrypted_size"]:
         assert crypt.encrypted_size(n) == e

@@ -80,3 +80,29 @@ def test_effective_cpus_follows_the_cgroup_quota(fake_sysfs, monkeypatch):
     assert lib.xs_effective_cpus() == min(aff, 2)
     monkeypatch.setenv("RCLONE_AMD_CPUS", "5")
     assert lib.xs_effective_cpus() == 5
+
+
+def test_effective_cpus_nested_cgroup_quota(fake_sysfs, tmp_path, monkeypatch):
+    """A process in a nested cgroup v2 group without a namespace (a systemd slice with
+    CPUQuota): the quota is the smallest cpu.max on the path from /proc/self/cgroup's group up to
+    the mount root, not only the root's file."""
+    import os
+    lib = _lib.lib()
+    aff = len(os.sched_getaffinity(0))
+    proc = tmp_path / "proc"
+    (proc / "self").mkdir(parents=True)
+    (proc / "self" / "cgroup").write_text("1:cpu:/\n0::/system.slice/rclone.service\n")
+    monkeypatch.setenv("RCLONE_AMD_PROC_ROOT", str(proc))
+    cg = fake_sysfs / "fs" / "cgroup"
+    (cg / "system.slice" / "rclone.service").mkdir(parents=True)
+    (cg / "system.slice" / "rclone.service" / "cpu.max").write_text("max 100000\n")
+    (cg / "system.slice" / "cpu.max").write_text("300000 100000\n")  # the slice: 3 CPUs
+    assert lib.xs_effective_cpus() == min(aff, 3)
+    (cg / "system.slice" / "rclone.service" / "cpu.max").write_text("100000 100000\n")  # tighter below
+    assert lib.xs_effective_cpus() == 1
+    (cg / "cpu.max").write_text("200000 100000\n")  # root looser than the group: the group wins
+    assert lib.xs_effective_cpus() == 1
+    (proc / "self" / "cgroup").write_text("0::/\n")  # a namespace: the root file only
+    assert lib.xs_effective_cpus() == min(aff, 2)
+    (proc / "self" / "cgroup").write_text("0::/../escape\n")  # never leaves the mount
+    assert lib.xs_effective_cpus() == min(aff, 2)

@@ -348,6 +348,7 @@ int main(int argc, char** argv) {
     close(fd);
   });
   const double t_gen = now() - tg0;
+  fprintf(stderr, "e2e: tree of %zu objects written in %.1f s\n", objs.size(), t_gen);
 
   int32_t err = 0;
   rc_cipher* c = rc_cipher_new("potato", "", &err);
@@ -521,6 +522,7 @@ int main(int argc, char** argv) {
       if (memcmp(objs[i].tee, objs[i].dst, 16)) bad++;
     });
     t_dst = now() - t0;
+    fprintf(stderr, "e2e: sync %.1f s, destination hash %.1f s\n", t_sync, t_dst);
     put_mismatch = bad;
   }
   // ---- cryptcheck: re-seal each local file with the stored nonce, MD5 on the GPU, compare
@@ -585,6 +587,7 @@ int main(int argc, char** argv) {
   t_names_dec = now() - tc0;
   cryptcheck(differ);
   const double t_check = now() - tc0, check_read = t_read, check_gpu = t_gpu;
+  fprintf(stderr, "e2e: cryptcheck %.1f s\n", t_check);
   uint64_t ndiff = 0;
   for (auto d : differ) ndiff += d;
   // ---- verify: decrypt sampled objects through rc_decrypt_data and compare with the files

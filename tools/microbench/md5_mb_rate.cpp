@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "../../rclone_amd/csrc/md5_x16.h"
+#include "md5_x8.h"
 #include "../../rclone_amd/csrc/xs_host_md5.h"
 
 static double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
