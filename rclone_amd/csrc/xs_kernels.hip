@@ -66,6 +66,15 @@
 #ifndef XS_OPEN_WPE
 #define XS_OPEN_WPE 1
 #endif
+#ifndef XS_LOAD_IMM  // the four staging loads of a group share one address (immediate offsets)
+#define XS_LOAD_IMM 0
+#endif
+#ifndef XS_MAD_COMBINE  // accumulator words combined by v_mad_u64_u32 (opaque byte weights)
+#define XS_MAD_COMBINE 0
+#endif
+#ifndef XS_LDS_XOR  // data XOR keystream done by LDS atomics on the staged words: 0 = VALU, 1 = data and
+#define XS_LDS_XOR 0  // Poly1305 sign bias both in LDS (no VALU XORs), 2 = data in LDS, bias on the VALU
+#endif
 
 
 namespace xs {
@@ -1425,10 +1434,21 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
     }
 #else
     uint32_t* sb = wb;
+#if XS_LOAD_IMM
+    // one 64-bit address per group: the four 1 KiB loads differ only in the instruction's
+    // immediate offset (no address VALU per load).  The hardware adds that offset to the LDS
+    // destination (M0) as well, so all four name the slot base and land 1 KiB apart.
+    const uint8_t* gsrc = pin_m32 + goff;
+    if (u > 0 || not_key) __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)sb, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)sb, 16, 1024, 0);
+    __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)sb, 16, 2048, 0);
+    __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)sb, 16, 3072, 0);
+#else
 #pragma unroll
     for (int j = 0; j < 4; j++)
       if (j > 0 || u > 0 || not_key)
         __builtin_amdgcn_global_load_lds(pin_m32 + goff + 1024 * j, (lds_void*)(sb + 256 * j), 16, 0, 0);
+#endif
 #endif
     uint32_t ks[16];
     salsa20_block_pre(pre, K, ks);
@@ -1439,6 +1459,62 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
     uint4* mine = reinterpret_cast<uint4*>(sb + 256 * (l >> 4) + 4 * (l & 15u));
+#if XS_LDS_XOR
+    static_assert(!XS_ST_PERM && !XS_DBUF, "LDS XOR works on the single staging slot");
+    // The data XOR runs on the LDS's own ALU: 64-bit atomic XORs on this lane's staged words, so
+    // the VALU issues no XOR for it.  Chunk j, half h of the lane sits at mine + 256 j + 8 h bytes.
+    // XS_LDS_XOR 1 also applies the MFMA operand's sign bias there (C = 0x80 in every byte):
+    //   seal: ^C, ^ks, then ^C returning d^ks^C = B (LDS ends as the ciphertext d^ks)
+    //   open: ^C, ^ks returning d^C = B, then ^C (LDS ends as the plaintext d^ks)
+    // XS_LDS_XOR 2 returns d from the ^ks pass and biases on the VALU.
+    typedef __attribute__((address_space(3))) uint64_t lds_u64;
+    lds_u64* m64 = (lds_u64*)mine;
+    uint64_t k64[8], r64[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) k64[q] = (uint64_t)ks[2 * q] | ((uint64_t)ks[2 * q + 1] << 32);
+    const uint64_t C64 = 0x8080808080808080ull;
+#define XS_AX(q, v) __hip_atomic_fetch_xor(m64 + 32 * ((q) >> 1) + ((q) & 1), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+#if XS_LDS_XOR == 1
+#pragma unroll
+    for (int q = 0; q < 8; q++) (void)XS_AX(q, C64);
+    if (SEAL) {
+#pragma unroll
+      for (int q = 0; q < 8; q++) (void)XS_AX(q, k64[q]);
+#pragma unroll
+      for (int q = 0; q < 8; q++) r64[q] = XS_AX(q, C64);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; q++) r64[q] = XS_AX(q, k64[q]);
+#pragma unroll
+      for (int q = 0; q < 8; q++) (void)XS_AX(q, C64);
+    }
+#else
+#pragma unroll
+    for (int q = 0; q < 8; q++) r64[q] = XS_AX(q, k64[q]);  // returns d
+#endif
+#undef XS_AX
+    asm volatile("" ::: "memory");  // LDS ops of one wave execute in order
+    {  // the staged words are now the output: out in load order
+      uint4 w[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) w[j] = *reinterpret_cast<const uint4*>(sb + 256 * j + 4 * l);
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (j > 0 || u > 0 || not_key) *reinterpret_cast<uint4*>(pout_m32 + goff + 1024 * j) = w[j];
+    }
+    uint32_t bw[16];  // the MFMA B words (biased ciphertext)
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+#if XS_LDS_XOR == 1
+      bw[2 * q] = (uint32_t)r64[q];
+      bw[2 * q + 1] = (uint32_t)(r64[q] >> 32);
+#else
+      const uint32_t d0 = (uint32_t)r64[q], d1 = (uint32_t)(r64[q] >> 32);
+      bw[2 * q] = SEAL ? (d0 ^ ks[2 * q] ^ 0x80808080u) : (d0 ^ 0x80808080u);
+      bw[2 * q + 1] = SEAL ? (d1 ^ ks[2 * q + 1] ^ 0x80808080u) : (d1 ^ 0x80808080u);
+#endif
+    }
+#else
     uint32_t d[16];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -1448,7 +1524,9 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
     uint32_t o[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) o[i] = d[i] ^ ks[i];
-#if XS_ST_PERM
+#endif
+#if XS_LDS_XOR
+#elif XS_ST_PERM
     {  // outputs leave in load order: 4x4 transpose of (16-lane row, chunk) with lane swaps --
        // afterwards register chunk j of lane λ holds chunk λ>>4 of lane 16j + (λ&15), i.e.
        // chunk 64j + perm(λ) of the group
@@ -1492,12 +1570,18 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
       A[1][i] = (int)__builtin_amdgcn_alignbyte(z[i + 1], z[i], zsh);
       A[0][i] = (int)__builtin_amdgcn_alignbyte(z[i + 5], z[i + 4], zsh);
     }
+#if !XS_LDS_XOR
     const uint32_t* cw = SEAL ? o : d;
+#endif
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       xs_v4i B;
 #pragma unroll
+#if XS_LDS_XOR
+      for (int i = 0; i < 4; i++) B[i] = (int)bw[4 * j + i];
+#else
       for (int i = 0; i < 4; i++) B[i] = (int)(cw[4 * j + i] ^ 0x80808080u);
+#endif
 #pragma unroll
       for (int mt = 0; mt < 2; mt++) {
         acc[j][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[mt], B, acc[j][mt], 0, 0, 0);
@@ -1529,13 +1613,20 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
   // ---- transpose the partial words through the (now free) staging slot: lane (n, kg) holds,
   // for column 4n + j, the words at 2^(32(4mt + kg)); lane λ finalises column 4(λ&15) + (λ>>4)
   uint64_t* t64 = reinterpret_cast<uint64_t*>(wb);
+  // the byte weights as opaque wave-uniform values: each term is then one v_mad_u64_u32 (a shift
+  // would be a zero-extend + 64-bit shift + 64-bit add)
+  uint32_t w8 = 1u << 8, w16 = 1u << 16, w24 = 1u << 24;
+#if XS_MAD_COMBINE
+  asm("" : "+s"(w8), "+s"(w16), "+s"(w24));
+#endif
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     uint64_t sx[2];
 #pragma unroll
     for (int mt = 0; mt < 2; mt++)
-      sx[mt] = (uint64_t)(uint32_t)acc[j][mt][0] + ((uint64_t)(uint32_t)acc[j][mt][1] << 8) +
-               ((uint64_t)(uint32_t)acc[j][mt][2] << 16) + ((uint64_t)(uint32_t)acc[j][mt][3] << 24);
+      sx[mt] = (uint64_t)(uint32_t)acc[j][mt][3] * w24 +
+               ((uint64_t)(uint32_t)acc[j][mt][2] * w16 +
+                ((uint64_t)(uint32_t)acc[j][mt][1] * w8 + (uint64_t)(uint32_t)acc[j][mt][0]));
     *reinterpret_cast<ulonglong2*>(t64 + (((n * 4u + j) * 4u + kg) * 2u)) = make_ulonglong2(sx[0], sx[1]);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
