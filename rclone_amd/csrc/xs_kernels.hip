@@ -33,6 +33,7 @@
 
 #include "xs_internal.h"
 #include "xs_salsa_lazy.h"
+#include "xs_salsa_r12.h"
 
 // XS_SEAL_WPE / XS_OPEN_WPE: minimum waves per SIMD the register allocator must allow
 // (amdgpu_waves_per_eu) for the seal / open kernels.
@@ -65,6 +66,9 @@
 #endif
 #ifndef XS_OPEN_WPE
 #define XS_OPEN_WPE 1
+#endif
+#ifndef XS_SALSA_R12  // double rounds 1-2 scheduled with the uniform words on the scalar unit (xs_salsa_r12.h)
+#define XS_SALSA_R12 0
 #endif
 #ifndef XS_LOAD_IMM  // the four staging loads of a group share one address (immediate offsets)
 #define XS_LOAD_IMM 0
@@ -225,6 +229,22 @@ __device__ __forceinline__ SalsaPre salsa_pre(const uint32_t (&k)[8], uint32_t n
 // Keystream block `ctr` from the precomputed first-round values (bit-identical to
 // salsa20_block).
 __device__ __forceinline__ void salsa20_block_pre(const SalsaPre& p, uint32_t ctr, uint32_t (&out)[16]) {
+#if XS_SALSA_R12
+  {  // double rounds 1-2 from the raw input words, uniform parts on the scalar unit (xs_salsa_r12.h)
+    const uint32_t w[16] = {SIG0, p.k[0], p.k[1], p.k[2], p.k[3], SIG1, p.n0, p.n1,
+                            ctr,  0u,     SIG2,   p.k[4], p.k[5], p.k[6], p.k[7], SIG3};
+    uint32_t b[16], t[16];
+    xs_salsa_r12(w, b, t);
+#pragma unroll 1
+    for (int i = 0; i < 8; i++) xs_salsa_dr_lazy(b, t);
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      if ((XS_LAZY_MASK >> i) & 1u) out[i] = xs_xad(b[i], t[i], w[i]);
+      else out[i] = b[i] + w[i];
+    }
+    return;
+  }
+#endif
   uint32_t x[16];
   // column QR(0,4,8,12) lane part
   x[8] = ctr ^ p.u9;
