@@ -25,3 +25,14 @@ def ref_kat():
 def sodium_vectors():
     with open(os.path.join(GOLDEN, "sodium_vectors.json")) as f:
         return json.load(f)
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    """Name the native library the run loaded (its build id = sha256 of the sources it was built
+    from, rclone_amd/build.py), last in the output so a log's tail carries it."""
+    try:
+        from rclone_amd import _lib
+        if _lib._lib is not None:
+            terminalreporter.write_line("rclone_amd library build id: " + _lib.build_id())
+    except Exception as exc:  # noqa: BLE001 -- never fail the run over the report line
+        terminalreporter.write_line(f"rclone_amd library build id unavailable: {exc}")
