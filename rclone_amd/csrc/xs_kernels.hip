@@ -33,7 +33,6 @@
 
 #include "xs_internal.h"
 #include "xs_salsa_lazy.h"
-#include "xs_salsa_r12.h"
 
 // XS_SEAL_WPE / XS_OPEN_WPE: minimum waves per SIMD the register allocator must allow
 // (amdgpu_waves_per_eu) for the seal / open kernels.
@@ -67,17 +66,8 @@
 #ifndef XS_OPEN_WPE
 #define XS_OPEN_WPE 1
 #endif
-#ifndef XS_SALSA_R12  // double rounds 1-2 scheduled with the uniform words on the scalar unit (xs_salsa_r12.h)
-#define XS_SALSA_R12 0
-#endif
-#ifndef XS_LOAD_IMM  // the four staging loads of a group share one address (immediate offsets)
-#define XS_LOAD_IMM 0
-#endif
-#ifndef XS_MAD_COMBINE  // accumulator words combined by v_mad_u64_u32 (opaque byte weights)
-#define XS_MAD_COMBINE 0
-#endif
-#ifndef XS_LDS_XOR  // data XOR keystream done by LDS atomics on the staged words: 0 = VALU, 1 = data and
-#define XS_LDS_XOR 0  // Poly1305 sign bias both in LDS (no VALU XORs), 2 = data in LDS, bias on the VALU
+#ifndef XS_LDS_XOR  // data XOR keystream and the MFMA operand's sign bias by LDS atomics on the staged
+#define XS_LDS_XOR 1  // words (1), or on the VALU (0)
 #endif
 
 
@@ -229,22 +219,6 @@ __device__ __forceinline__ SalsaPre salsa_pre(const uint32_t (&k)[8], uint32_t n
 // Keystream block `ctr` from the precomputed first-round values (bit-identical to
 // salsa20_block).
 __device__ __forceinline__ void salsa20_block_pre(const SalsaPre& p, uint32_t ctr, uint32_t (&out)[16]) {
-#if XS_SALSA_R12
-  {  // double rounds 1-2 from the raw input words, uniform parts on the scalar unit (xs_salsa_r12.h)
-    const uint32_t w[16] = {SIG0, p.k[0], p.k[1], p.k[2], p.k[3], SIG1, p.n0, p.n1,
-                            ctr,  0u,     SIG2,   p.k[4], p.k[5], p.k[6], p.k[7], SIG3};
-    uint32_t b[16], t[16];
-    xs_salsa_r12(w, b, t);
-#pragma unroll 1
-    for (int i = 0; i < 8; i++) xs_salsa_dr_lazy(b, t);
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      if ((XS_LAZY_MASK >> i) & 1u) out[i] = xs_xad(b[i], t[i], w[i]);
-      else out[i] = b[i] + w[i];
-    }
-    return;
-  }
-#endif
   uint32_t x[16];
   // column QR(0,4,8,12) lane part
   x[8] = ctr ^ p.u9;
@@ -1454,7 +1428,6 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
     }
 #else
     uint32_t* sb = wb;
-#if XS_LOAD_IMM
     // one 64-bit address per group: the four 1 KiB loads differ only in the instruction's
     // immediate offset (no address VALU per load).  The hardware adds that offset to the LDS
     // destination (M0) as well, so all four name the slot base and land 1 KiB apart.
@@ -1463,12 +1436,6 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
     __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)sb, 16, 1024, 0);
     __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)sb, 16, 2048, 0);
     __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)sb, 16, 3072, 0);
-#else
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-      if (j > 0 || u > 0 || not_key)
-        __builtin_amdgcn_global_load_lds(pin_m32 + goff + 1024 * j, (lds_void*)(sb + 256 * j), 16, 0, 0);
-#endif
 #endif
     uint32_t ks[16];
     salsa20_block_pre(pre, K, ks);
@@ -1481,12 +1448,13 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
     uint4* mine = reinterpret_cast<uint4*>(sb + 256 * (l >> 4) + 4 * (l & 15u));
 #if XS_LDS_XOR
     static_assert(!XS_ST_PERM && !XS_DBUF, "LDS XOR works on the single staging slot");
-    // The data XOR runs on the LDS's own ALU: 64-bit atomic XORs on this lane's staged words, so
-    // the VALU issues no XOR for it.  Chunk j, half h of the lane sits at mine + 256 j + 8 h bytes.
-    // XS_LDS_XOR 1 also applies the MFMA operand's sign bias there (C = 0x80 in every byte):
-    //   seal: ^C, ^ks, then ^C returning d^ks^C = B (LDS ends as the ciphertext d^ks)
-    //   open: ^C, ^ks returning d^C = B, then ^C (LDS ends as the plaintext d^ks)
-    // XS_LDS_XOR 2 returns d from the ^ks pass and biases on the VALU.
+    // The data XOR and the MFMA operand's sign bias (C = 0x80 in every byte) run on the LDS's own
+    // ALU: 64-bit atomic XORs on this lane's staged words, so the VALU issues no XOR for either
+    // (512 fewer VALU instructions per block; paired A/B in DESIGN.md section 3).  Chunk j, half h
+    // of the lane sits at mine + 256 j + 8 h bytes.
+    //   seal: ^C, ^ks, then ^C returning d^ks^C = B (the LDS ends as the ciphertext d^ks)
+    //   open: ^C, ^ks returning d^C = B, then ^C (the LDS ends as the plaintext d^ks)
+    // The group-0 key slots hold zeros, as with the VALU form.
     typedef __attribute__((address_space(3))) uint64_t lds_u64;
     lds_u64* m64 = (lds_u64*)mine;
     uint64_t k64[8], r64[8];
@@ -1494,7 +1462,6 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
     for (int q = 0; q < 8; q++) k64[q] = (uint64_t)ks[2 * q] | ((uint64_t)ks[2 * q + 1] << 32);
     const uint64_t C64 = 0x8080808080808080ull;
 #define XS_AX(q, v) __hip_atomic_fetch_xor(m64 + 32 * ((q) >> 1) + ((q) & 1), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-#if XS_LDS_XOR == 1
 #pragma unroll
     for (int q = 0; q < 8; q++) (void)XS_AX(q, C64);
     if (SEAL) {
@@ -1508,10 +1475,6 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
 #pragma unroll
       for (int q = 0; q < 8; q++) (void)XS_AX(q, C64);
     }
-#else
-#pragma unroll
-    for (int q = 0; q < 8; q++) r64[q] = XS_AX(q, k64[q]);  // returns d
-#endif
 #undef XS_AX
     asm volatile("" ::: "memory");  // LDS ops of one wave execute in order
     {  // the staged words are now the output: out in load order
@@ -1525,14 +1488,8 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
     uint32_t bw[16];  // the MFMA B words (biased ciphertext)
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-#if XS_LDS_XOR == 1
       bw[2 * q] = (uint32_t)r64[q];
       bw[2 * q + 1] = (uint32_t)(r64[q] >> 32);
-#else
-      const uint32_t d0 = (uint32_t)r64[q], d1 = (uint32_t)(r64[q] >> 32);
-      bw[2 * q] = SEAL ? (d0 ^ ks[2 * q] ^ 0x80808080u) : (d0 ^ 0x80808080u);
-      bw[2 * q + 1] = SEAL ? (d1 ^ ks[2 * q + 1] ^ 0x80808080u) : (d1 ^ 0x80808080u);
-#endif
     }
 #else
     uint32_t d[16];
@@ -1636,9 +1593,7 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
   // the byte weights as opaque wave-uniform values: each term is then one v_mad_u64_u32 (a shift
   // would be a zero-extend + 64-bit shift + 64-bit add)
   uint32_t w8 = 1u << 8, w16 = 1u << 16, w24 = 1u << 24;
-#if XS_MAD_COMBINE
   asm("" : "+s"(w8), "+s"(w16), "+s"(w24));
-#endif
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     uint64_t sx[2];
