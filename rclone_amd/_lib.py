@@ -158,7 +158,7 @@ def lib():
         want = _build.build_sources_sha256()
         have = _build.library_build_id(path)
         if have != want:
-            if os.environ.get("RCLONE_AMD_REBUILD", "1") == "0" or not os.path.exists(_build.HIPCC):
+            if os.environ.get("RCLONE_AMD_REBUILD", "1") == "0" or not _build.hipcc_available():
                 raise StaleLibraryError(
                     f"{path}: built from sources {have or 'unknown/missing'}, this tree is {want} "
                     "(rebuild: python -m rclone_amd.build)")

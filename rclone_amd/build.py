@@ -49,6 +49,11 @@ def kernel_sources_sha256(root=None):
     return h.hexdigest()
 
 
+def hipcc_available():
+    import shutil
+    return os.path.exists(HIPCC) or shutil.which(HIPCC) is not None
+
+
 def sources():
     return [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
 
