@@ -86,10 +86,17 @@ def launch_ranks(args):
     port = s.getsockname()[1]
     s.close()
     procs = []
+
+    def die_with_parent():  # a rank never outlives the launcher (a killed launcher must not leave
+        try:                # ranks waiting in a collective on the GPUs)
+            ctypes.CDLL(None).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except Exception:  # noqa: BLE001
+            pass
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      preexec_fn=die_with_parent))
 
     def stop(*_):
         for p in procs:
