@@ -1,13 +1,16 @@
+# Multi-rank rehearsal on a one-GPU box: bench.py --gpus N starts its own N ranks (gloo, sharing
+# the GPU) in every mode; each line must carry n_gpus = ranks_seen = N.  The same checks run in
+# the -m gpu suite (tests/test_dist_gpu.py); this script keeps the full-size lines.
 set -o pipefail
 mkdir -p gpurun_out
 export BENCH_DIST_BACKEND=gloo
-R="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
-timeout -k 10 300 $R --nproc-per-node 2 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 2 --no-cpu > gpurun_out/dist2.json 2> gpurun_out/dist2.err || { echo FAIL2; tail -30 gpurun_out/dist2.err; exit 1; }
-cat gpurun_out/dist2.json
-timeout -k 10 300 $R --nproc-per-node 4 --master-port 29512 bench.py --gpus 4 --steps 3 --warmup 2 --no-cpu > gpurun_out/dist4.json 2> gpurun_out/dist4.err || { echo FAIL4; tail -30 gpurun_out/dist4.err; exit 1; }
-cat gpurun_out/dist4.json
-timeout -k 10 300 $R --nproc-per-node 2 --master-port 29513 bench.py --gpus 2 --steps 2 --warmup 1 --object-blocks 400000 --no-cpu > gpurun_out/dist2_obj.json 2> gpurun_out/dist2_obj.err || { echo FAILOBJ; tail -30 gpurun_out/dist2_obj.err; exit 1; }
-cat gpurun_out/dist2_obj.json
-timeout -k 10 300 $R --nproc-per-node 2 --master-port 29514 bench.py --gpus 2 --steps 2 --warmup 1 --names 200000 --no-cpu > gpurun_out/dist2_names.json 2> gpurun_out/dist2_names.err || { echo FAILNAMES; tail -30 gpurun_out/dist2_names.err; exit 1; }
-cat gpurun_out/dist2_names.json
+run() {  # name, args...
+  local name=$1; shift
+  timeout -k 10 300 python bench.py --no-cpu "$@" > gpurun_out/$name.json 2> gpurun_out/$name.err || { echo FAIL $name; tail -30 gpurun_out/$name.err; exit 1; }
+  python3 -c "import json,sys; d=json.loads(open('gpurun_out/$name.json').read().strip().splitlines()[-1]); c=d['config']; assert d['n_gpus']==c['ranks_seen'], d; print('$name', d['value'], d['unit'], 'ranks_seen', c['ranks_seen'], 'distinct_gpus', c['distinct_gpus'])"
+}
+run dist2 --gpus 2 --steps 3 --warmup 2
+run dist4 --gpus 4 --steps 3 --warmup 2 --blocks 50000
+run dist2_obj --gpus 2 --steps 2 --warmup 1 --object-blocks 400000
+run dist2_names --gpus 2 --steps 2 --warmup 1 --names 200000
 echo REHEARSAL_DONE
