@@ -60,11 +60,11 @@
 #ifndef XS_XCD_REMAP
 #define XS_XCD_REMAP 0
 #endif
-#ifndef XS_SEAL_WPE
-#define XS_SEAL_WPE 1
+#ifndef XS_SEAL_WPE  // 5 waves per SIMD (<= 96 VGPRs): hides the LDS atomics' latency; paired
+#define XS_SEAL_WPE 5  // -0.7% seal / -1.1% open against 4
 #endif
 #ifndef XS_OPEN_WPE
-#define XS_OPEN_WPE 1
+#define XS_OPEN_WPE 5
 #endif
 #ifndef XS_LDS_XOR  // data XOR keystream and the MFMA operand's sign bias by LDS atomics on the staged
 #define XS_LDS_XOR 1  // words (1), or on the VALU (0)
