@@ -1588,7 +1588,12 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
           for (int i = 0; i < 4; i++) acc[j][mt][i] += (int)lds_all[(uint32_t)w * 2048u + (uint32_t)(8 * j + 4 * mt + i) * 64u + l];
   }
   // ---- transpose the partial words through the (now free) staging slot: lane (n, kg) holds,
-  // for column 4n + j, the words at 2^(32(4mt + kg)); lane λ finalises column 4(λ&15) + (λ>>4)
+  // for column 4n + j, the words at 2^(32(4mt + kg)); lane λ finalises column 4(λ&15) + (λ>>4).
+  // (ne, kge) = (n, kg) recomputed from an opaque copy of the lane id: kept live across the group
+  // loop instead, at five waves per SIMD the compiler spilled them to scratch.
+  uint32_t lid = threadIdx.x & 63u;
+  asm volatile("" : "+v"(lid));
+  const uint32_t ne = lid & 15u, kge = lid >> 4;
   uint64_t* t64 = reinterpret_cast<uint64_t*>(wb);
   // the byte weights as opaque wave-uniform values: each term is then one v_mad_u64_u32 (a shift
   // would be a zero-extend + 64-bit shift + 64-bit add)
@@ -1602,12 +1607,12 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
       sx[mt] = (uint64_t)(uint32_t)acc[j][mt][3] * w24 +
                ((uint64_t)(uint32_t)acc[j][mt][2] * w16 +
                 ((uint64_t)(uint32_t)acc[j][mt][1] * w8 + (uint64_t)(uint32_t)acc[j][mt][0]));
-    *reinterpret_cast<ulonglong2*>(t64 + (((n * 4u + j) * 4u + kg) * 2u)) = make_ulonglong2(sx[0], sx[1]);
+    *reinterpret_cast<ulonglong2*>(t64 + (((ne * 4u + j) * 4u + kge) * 2u)) = make_ulonglong2(sx[0], sx[1]);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   uint64_t x[8];
   {
-    const uint64_t* rd = t64 + (n * 4u + kg) * 8u;  // column 4n + kg: (kg', mt) pairs for kg' = 0..3
+    const uint64_t* rd = t64 + (ne * 4u + kge) * 8u;  // column 4n + kg: (kg', mt) pairs for kg' = 0..3
 #pragma unroll
     for (int kk = 0; kk < 4; kk++) {
       const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(rd + 2 * kk);
@@ -1618,7 +1623,7 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
   P5 hs;
   {
     const P5 V = column_value(x);
-    const uint32_t e = 66u - (4u * n + kg);  // column g = 4n + kg (this lane's column)
+    const uint32_t e = 66u - (4u * ne + kge);  // column g = 4n + kg (this lane's column)
     P5 t1, t2;
 #pragma unroll
     for (int i = 0; i < 5; i++) {
