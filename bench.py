@@ -65,6 +65,8 @@ def parse():
                     help="file-name mode (SURVEY 8(f) rank 4): encrypt + decrypt this many names per step "
                          "through rc_names_run (0 = the default crypt-block bench)")
     ap.add_argument("--name-paths", action="store_true", help="names mode: 3-segment paths instead of one segment")
+    ap.add_argument("--no-pool-check", action="store_true",
+                    help="skip the after-timing check of one process's engine pool over every visible GPU")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch check only: start the ranks, join the process group (gloo, CPU), all-reduce a "
                          "per-rank counter and print the line with value null; no device work")
@@ -275,6 +277,70 @@ def issue_bound(valu_insts, ms, clock_hz=None, mfma_insts=None):
         res.update({"window_clock_ghz": round(clock_hz / 1e9, 4), "peak_at_window_clock": round(peak_w, 1),
                     "frac_at_window_clock": round(achieved / peak_w, 4)})
     return res
+
+
+def pool_check(devices=None):
+    """After the timed region, rank 0 only, outside every timing: the drop-in's one-process spread
+    of objects over the node's GPUs (xs_pool over every visible device, the counterpart of
+    rclone's --transfers goroutine pool, fs/sync/sync.go:544-548).  A small batched put (crypt
+    files of 40 objects, 0 B .. 1 MiB) is split over the devices; every wire body and MD5 must equal
+    the CPU oracle's (checker only) and every device must have taken objects.  On a one-GPU box
+    it reports the device count and does nothing else.  Never fails the bench: errors are reported."""
+    import hashlib
+
+    import torch
+    n_dev = torch.cuda.device_count()
+    if devices is None:
+        if n_dev < 2:
+            return {"devices": n_dev, "ran": False}
+        devices = list(range(n_dev))
+    try:
+        from oracle import pyoracle as orc  # checker only, never timed
+        from rclone_amd import _lib, crypt
+        from rclone_amd.testdata import splitmix64_bytes
+        L = _lib.lib()
+        t0 = time.perf_counter()
+        pool = crypt.EnginePool(list(devices), batch_blocks=64)
+        try:
+            engines = [L.xs_engine_device(pool.engine(i)) for i in range(len(pool))]
+            key = splitmix64_bytes(0x9001, 32)
+            sizes = [0, 1, 65535, 65536, 65537, 1 << 20] + [20011 * k + 3 for k in range(1, 35)]
+            plains = [splitmix64_bytes(0x9100 + i, sz) for i, sz in enumerate(sizes)]
+            nonces = b"".join(splitmix64_bytes(0x9200 + i, 24) for i in range(len(sizes)))
+            offs, pos = [], 0
+            for sz in sizes:
+                offs.append(pos)
+                pos += (sz + 15) & ~15
+            stage = bytearray(pos + 16)
+            for o, p in zip(offs, plains):
+                stage[o:o + len(p)] = p
+            cnt = len(sizes)
+            u64s = ctypes.c_uint64 * cnt
+            lens_c, offs_c = u64s(*sizes), u64s(*offs)
+            total = L.xs_put_body_bytes(cnt, lens_c)
+            src = (ctypes.c_uint8 * len(stage)).from_buffer(stage)
+            body, md5 = (ctypes.c_uint8 * (total + 16))(), (ctypes.c_uint8 * (16 * cnt))()
+            rc = L.xs_pool_put_batch(pool.handle, key, cnt, nonces, offs_c, lens_c, src, body, md5)
+            if rc != 0:
+                return {"devices": n_dev, "ran": True, "ok": False, "error": _lib.last_error()}
+            raw, dig, bpos, bad = bytes(body), bytes(md5), 0, 0
+            for i, p in enumerate(plains):
+                want = orc.encrypt_file(p, nonces[24 * i:24 * i + 24], key)
+                bad += raw[bpos:bpos + len(want) - 32] != want[32:] or dig[16 * i:16 * i + 16] != hashlib.md5(want).digest()
+                bpos += (len(want) - 32 + 15) & ~15
+            took = []
+            for i in range(len(pool)):
+                st = (ctypes.c_uint64 * 3)()
+                L.xs_engine_md5_stats(pool.engine(i), st)
+                took.append(int(st[2]))  # objects this engine hashed
+        finally:
+            pool.close()
+        return {"devices": n_dev, "ran": True, "engine_devices": engines, "objects": cnt,
+                "objects_differing_from_oracle": int(bad), "engine_objects": took,
+                "ok": bad == 0 and all(t > 0 for t in took) and engines == list(devices),
+                "seconds": round(time.perf_counter() - t0, 3)}
+    except Exception as exc:  # noqa: BLE001 -- reported, never fatal to the bench line
+        return {"devices": n_dev, "ran": True, "ok": False, "error": repr(exc)[:300]}
 
 
 def run_objectset(args, world, rank, dev, dist):
@@ -840,6 +906,8 @@ def main():
         }
         if not args.no_cpu and world == 1:  # the CPU baseline is an N=1 figure (rank 0 only)
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        if not args.no_pool_check:
+            res["pool_check"] = pool_check()
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -141,3 +141,18 @@ def test_pool_over_distinct_devices():
         c.pool = None
     finally:
         pool.close()
+
+
+def test_bench_pool_check_runs_its_checks():
+    """bench.py's after-timing pool check (one process, engines over every visible GPU) on this
+    box's device repeated: the function the multi-GPU bench line runs, checked here for real."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    res = bench.pool_check([0, 0])
+    assert res["ran"] and res["ok"], res
+    assert res["engine_devices"] == [0, 0] and res["objects_differing_from_oracle"] == 0
+    assert all(t > 0 for t in res["engine_objects"])
+    if torch.cuda.device_count() < 2:
+        assert bench.pool_check() == {"devices": torch.cuda.device_count(), "ran": False}
