@@ -286,7 +286,7 @@ def pool_check(devices=None):
     files of 40 objects, 0 B .. 1 MiB) is split over the devices; every wire body and MD5 must equal
     the CPU oracle's (checker only) and every device must have taken objects.  On a one-GPU box
     it reports the device count and does nothing else.  Never fails the bench: errors are reported."""
-    import hashlib
+    import subprocess
 
     import torch
     n_dev = torch.cuda.device_count()
@@ -294,6 +294,25 @@ def pool_check(devices=None):
         if n_dev < 2:
             return {"devices": n_dev, "ran": False}
         devices = list(range(n_dev))
+    # in a child process with a time limit: whatever the pool does on a node it has never run
+    # on, the bench line still prints
+    code = ("import json, sys; sys.path.insert(0, %r); import bench; "
+            "print(json.dumps(bench._pool_check_body(%r)))" % (ROOT, list(devices)))
+    try:
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT)
+    except subprocess.TimeoutExpired:
+        return {"devices": n_dev, "ran": True, "ok": False, "error": "timed out after 120 s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"devices": n_dev, "ran": True, "ok": False, "error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+    return json.loads(lines[-1])
+
+
+def _pool_check_body(devices):
+    import hashlib
+
+    import torch
+    n_dev = torch.cuda.device_count()
     try:
         from oracle import pyoracle as orc  # checker only, never timed
         from rclone_amd import _lib, crypt
