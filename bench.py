@@ -20,6 +20,7 @@ import argparse
 import ctypes
 import json
 import os
+import socket
 import sys
 import time
 
@@ -122,6 +123,26 @@ def launch_ranks(args):
     return rc
 
 
+def grouped(world):
+    """Whether this run holds a process group: every N > 1 run, and an N = 1 run under
+    BENCH_FORCE_PG=1, which puts the one rank through the same RCCL calls an N-GPU run makes
+    (init with device_id, the topology gather, barriers, counter SUM and time MAX all-reduces):
+    the RCCL path's rehearsal on a one-GPU box, where two RCCL ranks cannot share the device."""
+    return world > 1 or os.environ.get("BENCH_FORCE_PG") == "1"
+
+
+def force_pg_env(world):
+    """The env:// rendezvous a one-rank group under BENCH_FORCE_PG needs when no launcher set it."""
+    if world == 1:
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+
+
 def rank_topology(dist, world, dev):
     """What the job actually ran on: the process group's own world size and each rank's GPU
     (PCI domain:bus:device, gathered with one small all-reduce).  `distinct_gpus` < ranks means
@@ -129,7 +150,7 @@ def rank_topology(dist, world, dev):
     import torch
     p = torch.cuda.get_device_properties(dev)
     me = (p.pci_domain_id << 16) | (p.pci_bus_id << 8) | p.pci_device_id
-    if world == 1:
+    if not grouped(world):
         ids = [me]
         seen = 1
     else:
@@ -139,22 +160,24 @@ def rank_topology(dist, world, dev):
         dist.all_reduce(t)
         ids = [int(x) for x in t.cpu().tolist()]
     bus = ["%04x:%02x:%02x" % (i >> 16, (i >> 8) & 0xFF, i & 0xFF) for i in ids]
-    return {"ranks_seen": seen, "rank_gpus": bus, "distinct_gpus": len(set(ids))}
+    return {"ranks_seen": seen, "rank_gpus": bus, "distinct_gpus": len(set(ids)),
+            "process_group": dist.get_backend() if grouped(world) else None}
 
 
 def run_dry(args, world, rank, dist):
     """--dry-run: the launch and the collective without any device work (CPU test of N > 1)."""
     import torch
-    seen = dist.get_world_size() if world > 1 else 1
+    seen = dist.get_world_size() if grouped(world) else 1
     t = torch.tensor([1, rank], dtype=torch.int64)
-    if world > 1:
+    if grouped(world):
         dist.all_reduce(t)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "dry_run": True,
-                          "config": {"ranks_seen": seen, "ranks_reported": int(t[0]), "rank_sum": int(t[1])}}),
+                          "config": {"ranks_seen": seen, "ranks_reported": int(t[0]), "rank_sum": int(t[1]),
+                                     "process_group": dist.get_backend() if grouped(world) else None}}),
               flush=True)
-    if world > 1:
+    if grouped(world):
         dist.destroy_process_group()
 
 
@@ -376,20 +399,20 @@ def run_objectset(args, world, rank, dev, dist):
         r.run_round(0)
     torch.cuda.synchronize(dev)
     r.counters.zero_()
-    if world > 1:
+    if grouped(world):
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         r.run_all(record=True)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if grouped(world):
         dist.barrier()
     el = time.perf_counter() - t0
     counters = r.counters.clone()
     tmax = torch.tensor([el], dtype=torch.float64, device=dev)
-    shard.reduce_counters(counters, dist if world > 1 else None)
-    if world > 1:
+    shard.reduce_counters(counters, dist if grouped(world) else None)
+    if grouped(world):
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     el = float(tmax.item())
     blocks, nbytes, fails, mism, d0, d1 = digest_to_u64(counters)
@@ -418,7 +441,7 @@ def run_objectset(args, world, rank, dev, dist):
             "roofline": None, "cpu_baseline": None,
         }
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if grouped(world):
         dist.destroy_process_group()
 
 
@@ -510,7 +533,7 @@ def run_mixed(args, world, rank, dev, dist):
         open_()
     torch.cuda.synchronize(dev)
     ev = []
-    if world > 1:
+    if grouped(world):
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -518,7 +541,7 @@ def run_mixed(args, world, rank, dev, dist):
         seal(wire_b, ev)
         open_(ev)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if grouped(world):
         dist.barrier()
     el = time.perf_counter() - t0
     # verification after the timed region: exactly the tampered blocks fail, are zero-filled, the
@@ -534,8 +557,8 @@ def run_mixed(args, world, rank, dev, dist):
     counters = torch.tensor([args.steps * 2 * nb, args.steps * 2 * int(d["len"].sum()), len(fails),
                              0 if good else 1], dtype=torch.int64, device=dev)
     tmax = torch.tensor([el], dtype=torch.float64, device=dev)
-    shard.reduce_counters(counters, dist if world > 1 else None)
-    if world > 1:
+    shard.reduce_counters(counters, dist if grouped(world) else None)
+    if grouped(world):
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     el = float(tmax.item())
     if int(counters[3].item()):
@@ -575,7 +598,7 @@ def run_mixed(args, world, rank, dev, dist):
             "cpu_baseline": None,
         }
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if grouped(world):
         dist.destroy_process_group()
 
 
@@ -653,7 +676,7 @@ def run_names(args, world, rank):
     for _ in range(args.warmup):
         L.rc_names_free(run(op_e, pa, pl))
         L.rc_names_free(run(op_d, ea, el_))
-    if world > 1:
+    if grouped(world):
         import torch.distributed as dist
         dist.barrier()
     k_e, k_d, t_e, t_d = [], [], [], []
@@ -670,7 +693,7 @@ def run_names(args, world, rank):
         t_e.append(b - a)
         t_d.append(time.perf_counter() - b)
     el = time.perf_counter() - t0
-    if world > 1:
+    if grouped(world):
         import torch.distributed as dist
         t = torch.tensor([el], dtype=torch.float64, device="cuda")  # RCCL reduces device tensors only
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -698,7 +721,7 @@ def run_names(args, world, rank):
         if not args.no_cpu and world == 1:  # the CPU baseline is an N=1 figure (rank 0 only)
             res["cpu_baseline"] = names_cpu_baseline(segs, c.name_key, c.name_tweak, 5.0)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if grouped(world):
         import torch.distributed as dist
         dist.destroy_process_group()
 
@@ -723,7 +746,8 @@ def main():
     # rank per GPU.
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
     if args.dry_run:
-        if world > 1:
+        if grouped(world):
+            force_pg_env(world)
             dist.init_process_group("gloo")
         return run_dry(args, world, rank, dist)
     ndev = torch.cuda.device_count()
@@ -733,7 +757,8 @@ def main():
     gpu = local % max(ndev, 1) if backend == "gloo" else local
     # the C library's engines (rc_* handles, file names) run on this rank's GPU too
     os.environ.setdefault("RCLONE_AMD_DEVICE", str(gpu))
-    if world > 1:
+    if grouped(world):
+        force_pg_env(world)
         torch.cuda.set_device(gpu)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
@@ -829,7 +854,7 @@ def main():
             w = body[i * BLOCK_SIZE:(i + 1) * BLOCK_SIZE].cpu().numpy().tobytes()
             if orc.seal(p, block_nonce[j], key) != w:
                 raise SystemExit("bench: block %d differs from the oracle" % i)
-    if world > 1:
+    if grouped(world):
         dist.barrier()
     # the clock probe runs at N=1 only (RCCL's own streams could share its hardware queue)
     probe = ClockProbe(L, dev) if world == 1 else None
@@ -840,7 +865,7 @@ def main():
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if grouped(world):
         dist.barrier()
     el = time.perf_counter() - t0
     clock = probe.result() if probe else None
@@ -852,8 +877,8 @@ def main():
                             dtype=torch.int64, device=dev)
     counters[3:5] = tag_digest(body, nb)  # order-independent: the same for any world size
     tmax = torch.tensor([el], dtype=torch.float64, device=dev)
-    shard.reduce_counters(counters, dist if world > 1 else None)
-    if world > 1:
+    shard.reduce_counters(counters, dist if grouped(world) else None)
+    if grouped(world):
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     el = float(tmax.item())
     seal_ms = [a.elapsed_time(b) for s, a, b in ev if s]
@@ -928,7 +953,7 @@ def main():
         if not args.no_pool_check:
             res["pool_check"] = pool_check()
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if grouped(world):
         dist.destroy_process_group()
 
 

@@ -113,6 +113,6 @@ def mixed_object_layout(total, rng, min_size=4096, max_size=8 << 20):
 
 def reduce_counters(counters, dist=None, group=None):
     """Sum a small int64 tensor of counters over all ranks (the only collective)."""
-    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist is not None and dist.is_initialized():
         dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
     return counters

@@ -103,7 +103,18 @@ def test_bench_starts_its_own_ranks():
     assert len(lines) == 1, r.stdout
     res = lines[0]
     assert res["n_gpus"] == 2 and res["dry_run"] is True
-    assert res["config"] == {"ranks_seen": 2, "ranks_reported": 2, "rank_sum": 1}
+    assert res["config"] == {"ranks_seen": 2, "ranks_reported": 2, "rank_sum": 1, "process_group": "gloo"}
+
+
+def test_bench_forced_one_rank_group():
+    """BENCH_FORCE_PG=1 puts an N = 1 run through a one-rank process group (its own rendezvous on
+    127.0.0.1 when no launcher set one): the collectives an N-GPU run makes, on one rank."""
+    r, lines = _bench(["--dry-run", "--steps", "1"], {"BENCH_FORCE_PG": "1"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 1
+    assert lines[0]["config"] == {"ranks_seen": 1, "ranks_reported": 1, "rank_sum": 0, "process_group": "gloo"}
+    r, lines = _bench(["--dry-run", "--steps", "1"])
+    assert r.returncode == 0 and lines[0]["config"]["process_group"] is None
 
 
 def test_bench_refuses_gpus_world_mismatch():

@@ -29,11 +29,12 @@ def need_gpu():
         pytest.skip("no HIP device")
 
 
-def _bench(*args, gloo=True):
+def _bench(*args, gloo=True, env_extra=None):
     env = {k: v for k, v in os.environ.items()
-           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "BENCH_FORCE_PG")}
     if gloo:
         env["BENCH_DIST_BACKEND"] = "gloo"
+    env.update(env_extra or {})
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--warmup-seconds", "0", "--no-cpu", *args],
                        capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -72,6 +73,28 @@ def test_bench_two_ranks_names_and_mixed():
     assert names["n_gpus"] == 2 and names["config"]["ranks_seen"] == 2 and names["value"] > 0
     mixed = _bench("--gpus", "2", "--steps", "1", "--warmup", "1", "--mixed-gib", "0.1")
     assert mixed["n_gpus"] == 2 and mixed["counters"]["verified"] is True
+
+
+def test_bench_rccl_one_rank_group_matches_no_group():
+    """Every RCCL call the N-GPU line makes (init with device_id, the topology gather, barriers,
+    the counter SUM and the time MAX all-reduces, destroy), run for real on this box's GPU through
+    a one-rank RCCL group (BENCH_FORCE_PG=1; two RCCL ranks cannot share one device), in each
+    mode: the results equal the run without a group."""
+    base = ["--gpus", "1", "--steps", "2", "--warmup", "1"]
+    for extra in (["--blocks", "8192"], ["--object-blocks", "40000", "--blocks", "8192"], ["--names", "20000"],
+                  ["--mixed-gib", "0.1"]):
+        pg = _bench(*base, *extra, gloo=False, env_extra={"BENCH_FORCE_PG": "1", "BENCH_DIST_BACKEND": "nccl"})
+        assert pg["config"]["process_group"] == "nccl" and pg["config"]["ranks_seen"] == 1, (extra, pg["config"])
+        assert pg["n_gpus"] == 1 and pg["value"] > 0
+        if "--names" in extra:
+            continue
+        one = _bench(*base, *extra, gloo=False)
+        assert one["config"]["process_group"] is None
+        if "--mixed-gib" in extra:
+            assert pg["counters"]["verified"] is True
+            continue
+        for k in ("blocks", "bytes", "tag_failures", "tag_digest"):
+            assert pg["counters"][k] == one["counters"][k], (extra, k)
 
 
 def test_bench_rccl_refuses_more_ranks_than_gpus():
