@@ -20,7 +20,6 @@ import argparse
 import ctypes
 import json
 import os
-import socket
 import sys
 import time
 
@@ -58,6 +57,11 @@ def parse():
                     help="configs[3] mode: one logical object of this many blocks (2^24 = 1 TiB) split "
                          "round-robin over the ranks, processed in --blocks rounds with on-device "
                          "generation inside each step (0 = the default resident-set bench)")
+    ap.add_argument("--objectset-steps", type=int, default=3,
+                    help="after the headline timing: the configs[3] leg (the 2^24-block 1 TiB object round-robin "
+                         "over the ranks, generate + seal + open + verify), this many timed steps after "
+                         "--objectset-warmup untimed ones; reported as the line's `objectset` key (0 = skip)")
+    ap.add_argument("--objectset-warmup", type=int, default=1)
     ap.add_argument("--mixed-gib", type=float, default=0.0,
                     help="configs[2] mode: this many GiB of 4 KiB-8 MiB objects per rank (descriptor batches, "
                          "partial last blocks, ~0.1%% of the blocks tampered); one step = seal the set + "
@@ -79,15 +83,19 @@ def launch_ranks(args):
     process per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), and exit
     with the first non-zero rank status (the other ranks are then stopped by PID).  Runs before
     anything touches the GPU: the children are fresh interpreters, never an exec of this one.
-    Only rank 0 prints the JSON line."""
+    Only rank 0 prints the JSON line.
+
+    The rendezvous store is hosted here, by the launcher, for the job's whole life (as torchrun's
+    agent does): its port is bound once and never released before the ranks connect, so no other
+    process can take it in between; the ranks are told to be clients of it
+    (TORCHELASTIC_USE_AGENT_STORE).  The launcher never touches a GPU."""
     import signal
-    import socket
     import subprocess
+
+    from torch.distributed import TCPStore
     n = args.gpus
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    store = TCPStore("127.0.0.1", 0, n, is_master=True, wait_for_workers=False)
+    port = store.port
     procs = []
 
     def die_with_parent():  # a rank never outlives the launcher (a killed launcher must not leave
@@ -97,7 +105,8 @@ def launch_ranks(args):
             pass
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   TORCHELASTIC_USE_AGENT_STORE="True")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       preexec_fn=die_with_parent))
 
@@ -120,6 +129,7 @@ def launch_ranks(args):
                       file=sys.stderr, flush=True)
                 stop()
         time.sleep(0.02)
+    del store
     return rc
 
 
@@ -131,16 +141,15 @@ def grouped(world):
     return world > 1 or os.environ.get("BENCH_FORCE_PG") == "1"
 
 
-def force_pg_env(world):
-    """The env:// rendezvous a one-rank group under BENCH_FORCE_PG needs when no launcher set it."""
-    if world == 1:
-        os.environ.setdefault("RANK", "0")
-        os.environ.setdefault("WORLD_SIZE", "1")
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if "MASTER_PORT" not in os.environ:
-            with socket.socket() as s:
-                s.bind(("127.0.0.1", 0))
-                os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+def pg_init_kwargs(world):
+    """init_process_group arguments.  Under a launcher: env:// (nothing to add).  A one-rank group
+    under BENCH_FORCE_PG with no launcher: an in-process store on a port bound once and kept
+    (no bind-close-rebind window for another process to take the port)."""
+    if world == 1 and "MASTER_PORT" not in os.environ:
+        from torch.distributed import TCPStore
+        return {"store": TCPStore("127.0.0.1", 0, 1, is_master=True, wait_for_workers=False),
+                "rank": 0, "world_size": 1}
+    return {}
 
 
 def rank_topology(dist, world, dev):
@@ -302,6 +311,12 @@ def issue_bound(valu_insts, ms, clock_hz=None, mfma_insts=None):
     return res
 
 
+def pool_check_timeout(n_devices):
+    """Seconds the pool-check child may take: a base for interpreter start, torch import and the
+    oracle check, plus a share per engine (device context + streams + staging)."""
+    return 90 + 15 * max(1, n_devices)
+
+
 def pool_check(devices=None):
     """After the timed region, rank 0 only, outside every timing: the drop-in's one-process spread
     of objects over the node's GPUs (xs_pool over every visible device, the counterpart of
@@ -318,13 +333,15 @@ def pool_check(devices=None):
             return {"devices": n_dev, "ran": False}
         devices = list(range(n_dev))
     # in a child process with a time limit: whatever the pool does on a node it has never run
-    # on, the bench line still prints
+    # on, the bench line still prints.  The limit grows with the device count (each engine opens
+    # its device's context and streams; a cold context costs seconds on a fresh node).
     code = ("import json, sys; sys.path.insert(0, %r); import bench; "
             "print(json.dumps(bench._pool_check_body(%r)))" % (ROOT, list(devices)))
+    limit = pool_check_timeout(len(devices))
     try:
-        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT)
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=limit, cwd=ROOT)
     except subprocess.TimeoutExpired:
-        return {"devices": n_dev, "ran": True, "ok": False, "error": "timed out after 120 s"}
+        return {"devices": n_dev, "ran": True, "ok": False, "error": f"timed out after {limit} s"}
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
         return {"devices": n_dev, "ran": True, "ok": False, "error": f"rc {r.returncode}: {r.stderr[-300:]}"}
@@ -385,25 +402,22 @@ def _pool_check_body(devices):
         return {"devices": n_dev, "ran": True, "ok": False, "error": repr(exc)[:300]}
 
 
-def run_objectset(args, world, rank, dev, dist):
-    """BASELINE configs[3]: the rank's round-robin share of an --object-blocks object, in
-    --blocks rounds; one step = every round (generate in HBM, seal, open, verify, digest)."""
+def time_objectset(r, steps, warm, world, dev, dist):
+    """Time `steps` full passes of a RankRunner (every round: generate in HBM, seal, open, verify,
+    digest) after `warm()`, bracketed by barrier + synchronize on both sides; counters summed and
+    the time max-reduced over the ranks.  Returns (seconds, summed counters, kernel ms lists)."""
     import torch
 
     from rclone_amd import shard
-    from rclone_amd.objectset import RankRunner, digest_to_u64
-    key = bytes(range(32))
-    nonce0 = bytes([0xF0]) + bytes([0xFF] * 7) + bytes(16)
-    r = RankRunner(key, nonce0, args.object_blocks, world, rank, args.blocks, 0x5EED, dev)
-    for _ in range(args.warmup):
-        r.run_round(0)
+    warm()
     torch.cuda.synchronize(dev)
     r.counters.zero_()
+    r.kernel_events.clear()
     if grouped(world):
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         r.run_all(record=True)
     torch.cuda.synchronize(dev)
     if grouped(world):
@@ -414,12 +428,63 @@ def run_objectset(args, world, rank, dev, dist):
     shard.reduce_counters(counters, dist if grouped(world) else None)
     if grouped(world):
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    el = float(tmax.item())
+    seal_ms = [a.elapsed_time(b) for s, a, b in r.kernel_events if s]
+    open_ms = [a.elapsed_time(b) for s, a, b in r.kernel_events if not s]
+    return float(tmax.item()), counters, seal_ms, open_ms
+
+
+def objectset_leg(args, world, rank, dev, dist):
+    """The headline run's configs[3] leg, after the headline timing and outside it: BASELINE
+    configs[3]'s 1 TiB object (2^24 blocks, block g sealed with nonce0 + g, cipher.go:665-678)
+    round-robin over the N ranks in 100k-block rounds, the same object set
+    tests/test_objectset_gpu.py runs (rclone_amd.objectset.CONFIG3_*), so the tag digest here must
+    equal the one that test prints for world 1, 2 and 8.  Fixed total work: strong scaling.
+    All ranks run it; rank 0 gets the dict, the others None."""
+    import torch
+
+    from rclone_amd.objectset import (CONFIG3_BLOCKS, CONFIG3_KEY, CONFIG3_NONCE0, CONFIG3_ROUND_BLOCKS,
+                                      CONFIG3_SEED, RankRunner, digest_to_u64)
+    total = int(os.environ.get("BENCH_OBJECTSET_BLOCKS", CONFIG3_BLOCKS))
+    t_setup = time.perf_counter()
+    r = RankRunner(CONFIG3_KEY, CONFIG3_NONCE0, total, world, rank, CONFIG3_ROUND_BLOCKS, CONFIG3_SEED, dev)
+    setup_s = time.perf_counter() - t_setup
+
+    def warm():
+        for _ in range(args.objectset_warmup):
+            r.run_all()
+    el, counters, seal_ms, open_ms = time_objectset(r, args.objectset_steps, warm, world, dev, dist)
+    blocks, nbytes, fails, mism, d0, d1 = digest_to_u64(counters)
+    ok = fails == 0 and mism == 0 and blocks == args.objectset_steps * total
+    del r
+    torch.cuda.empty_cache()
+    if rank != 0:
+        return None
+    return {"workload": f"BASELINE configs[3]: one {total}-block object ({total * BLOCK_DATA / 2**40:.3f} TiB) "
+                        f"round-robin over {world} rank(s), {CONFIG3_ROUND_BLOCKS}-block rounds; one step = "
+                        "generate in HBM + seal + open + verify every block",
+            "value": round(2 * nbytes / 2**30 / el, 3), "unit": "GiB/s", "scaling": "strong",
+            "steps": args.objectset_steps, "warmup": args.objectset_warmup,
+            "ms_per_step": round(el / args.objectset_steps * 1e3, 3), "ok": ok,
+            "seal_kernel_ms_avg": round(sum(seal_ms) / max(len(seal_ms), 1), 4),
+            "open_kernel_ms_avg": round(sum(open_ms) / max(len(open_ms), 1), 4),
+            "setup_s": round(setup_s, 2),
+            "counters": {"blocks": blocks, "bytes": nbytes, "tag_failures": fails, "roundtrip_mismatch_words": mism,
+                         "tag_digest": f"{d1:016x}{d0:016x}"}}
+
+
+def run_objectset(args, world, rank, dev, dist):
+    """BASELINE configs[3]: the rank's round-robin share of an --object-blocks object, in
+    --blocks rounds; one step = every round (generate in HBM, seal, open, verify, digest)."""
+    from rclone_amd.objectset import CONFIG3_KEY, CONFIG3_NONCE0, CONFIG3_SEED, RankRunner, digest_to_u64
+    r = RankRunner(CONFIG3_KEY, CONFIG3_NONCE0, args.object_blocks, world, rank, args.blocks, CONFIG3_SEED, dev)
+
+    def warm():
+        for _ in range(args.warmup):
+            r.run_round(0)
+    el, counters, seal_ms, open_ms = time_objectset(r, args.steps, warm, world, dev, dist)
     blocks, nbytes, fails, mism, d0, d1 = digest_to_u64(counters)
     if fails or mism or blocks != args.steps * args.object_blocks:
         raise SystemExit(f"bench: object set failed (blocks {blocks}, tag failures {fails}, mismatches {mism})")
-    seal_ms = [a.elapsed_time(b) for s, a, b in r.kernel_events if s]
-    open_ms = [a.elapsed_time(b) for s, a, b in r.kernel_events if not s]
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -747,8 +812,7 @@ def main():
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
     if args.dry_run:
         if grouped(world):
-            force_pg_env(world)
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", **pg_init_kwargs(world))
         return run_dry(args, world, rank, dist)
     ndev = torch.cuda.device_count()
     if backend == "nccl" and world > 1 and ndev < world:
@@ -758,12 +822,11 @@ def main():
     # the C library's engines (rc_* handles, file names) run on this rank's GPU too
     os.environ.setdefault("RCLONE_AMD_DEVICE", str(gpu))
     if grouped(world):
-        force_pg_env(world)
         torch.cuda.set_device(gpu)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu), **pg_init_kwargs(world))
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, **pg_init_kwargs(world))
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
     from rclone_amd import _lib
@@ -883,6 +946,8 @@ def main():
     el = float(tmax.item())
     seal_ms = [a.elapsed_time(b) for s, a, b in ev if s]
     open_ms = [a.elapsed_time(b) for s, a, b in ev if not s]
+    # configs[3] leg: every rank, after the headline's timing and reduction (never inside them)
+    objset = objectset_leg(args, world, rank, dev, dist) if args.objectset_steps > 0 else None
     if os.environ.get("BENCH_TRACE"):
         print("seal_ms", [round(x, 3) for x in seal_ms], "\nopen_ms", [round(x, 3) for x in open_ms],
               file=sys.stderr)
@@ -947,14 +1012,18 @@ def main():
                          "tag_digest": "%016x%016x" % (int(counters[4].item()) & (2**64 - 1),
                                                        int(counters[3].item()) & (2**64 - 1))},
             "cpu_baseline": None,
+            "objectset": objset,
         }
+    # the group is torn down before rank 0's after-timing checks: the other ranks leave (and free
+    # their GPUs) instead of waiting in the group while the pool check opens every device
+    if grouped(world):
+        dist.destroy_process_group()
+    if rank == 0:
         if not args.no_cpu and world == 1:  # the CPU baseline is an N=1 figure (rank 0 only)
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         if not args.no_pool_check:
             res["pool_check"] = pool_check()
         print(json.dumps(res), flush=True)
-    if grouped(world):
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

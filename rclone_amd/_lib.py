@@ -149,20 +149,19 @@ class StaleLibraryError(RuntimeError):
 
 def lib():
     """Load the native library built from this tree's sources.  A library whose embedded build id
-    differs from the tree's (rclone_amd/build.py build_sources_sha256) is rebuilt, or refused
-    with StaleLibraryError when RCLONE_AMD_REBUILD=0 or no hipcc is present; a library missing
+    differs from the tree's (rclone_amd/build.py build_sources_sha256), or that another installed
+    hipcc built (build.stale_reason), is rebuilt, or refused with StaleLibraryError when
+    RCLONE_AMD_REBUILD=0 or no hipcc is present; a library missing
     any declared entry point is refused too.  Never a fallback."""
     global _lib
     if _lib is None:
         path = _build.LIB
         want = _build.build_sources_sha256()
-        have = _build.library_build_id(path)
-        if have != want:
+        why = _build.stale_reason(path)
+        if why is not None:
             if os.environ.get("RCLONE_AMD_REBUILD", "1") == "0" or not _build.hipcc_available():
-                raise StaleLibraryError(
-                    f"{path}: built from sources {have or 'unknown/missing'}, this tree is {want} "
-                    "(rebuild: python -m rclone_amd.build)")
-            _build.build()
+                raise StaleLibraryError(f"{path}: {why} (rebuild: python -m rclone_amd.build)")
+            _build.build()  # under the build lock: concurrent callers build once
         if not os.path.exists(path):
             raise RuntimeError(f"rclone_amd native library missing: {path}")
         L = ctypes.CDLL(path)

@@ -8,7 +8,10 @@ Provenance: every build embeds `build_sources_sha256()` -- the sha256 of every f
 csrc/, the public header and the compile command -- as the library's build id
 (`xs_build_id()`, and a tagged string the loader reads from the file without loading it).
 `needs_build()` compares that id with the tree's, not file times, so a library built from other
-sources is never taken for this tree's (rclone_amd/_lib.py rebuilds or refuses it).
+sources is never taken for this tree's (rclone_amd/_lib.py rebuilds or refuses it).  The compiler
+is stamped beside it (`compiler_id()`: a digest of `hipcc --version`, tag "xs-build-compiler:"): where
+hipcc is installed, a library built by another hipcc / ROCm counts as stale too.  It is kept out of
+the build id so a box without a compiler can still load the library it was given.
 """
 import fcntl
 import hashlib
@@ -29,6 +32,8 @@ SOURCES = ["xs_kernels.hip", "xs_md5.hip", "xs_eme.hip", "xs_probe.hip", "xs_api
            "names_gpu.cpp", "scrypt.cpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-result"]
 BUILD_ID_TAG = b"xs-build-id:"
+COMPILER_TAG = b"xs-build-compiler:"
+_compiler_id = None
 
 
 # what the crypt kernels (xs_seal / xs_open / keygen) are compiled from: PMC counters committed under
@@ -87,8 +92,45 @@ def library_build_id(path=LIB):
     return m.group(1).decode() if m else None
 
 
+def compiler_id():
+    """First 16 hex digits of sha256(`$HIPCC --version`), or None without a usable hipcc."""
+    global _compiler_id
+    if _compiler_id is None:
+        try:
+            out = subprocess.run([HIPCC, "--version"], capture_output=True, timeout=60).stdout
+        except (OSError, subprocess.SubprocessError):
+            return None
+        if not out:
+            return None
+        _compiler_id = hashlib.sha256(out).hexdigest()[:16]
+    return _compiler_id
+
+
+def library_compiler_id(path=LIB):
+    """The compiler digest stamped into a built library file (None if absent or unstamped)."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    m = re.search(re.escape(COMPILER_TAG) + rb"([0-9a-f]{16})\0", data)
+    return m.group(1).decode() if m else None
+
+
+def stale_reason(path=LIB):
+    """Why the library at `path` is not this tree's build (None when it is): its build id differs
+    from the tree's sources, or -- where hipcc is installed -- another compiler built it."""
+    have, want = library_build_id(path), build_sources_sha256()
+    if have != want:
+        return f"built from sources {have or 'unknown/missing'}, this tree is {want}"
+    cc = compiler_id() if hipcc_available() else None
+    if cc is not None and library_compiler_id(path) != cc:
+        return f"built by compiler {library_compiler_id(path) or 'unstamped'}, installed hipcc is {cc}"
+    return None
+
+
 def needs_build():
-    return library_build_id(LIB) != build_sources_sha256()
+    return stale_reason(LIB) is not None
 
 
 def build(force=False, verbose=False):
@@ -100,6 +142,7 @@ def build(force=False, verbose=False):
         if not force and not needs_build():
             return LIB
         bid = build_sources_sha256()
+        cc = compiler_id() or "unstamped"
         tmp = f"{LIB}.tmp{os.getpid()}"
         # one object per source, compiled in parallel (xs_kernels.hip alone is most of the time),
         # then one link
@@ -109,7 +152,7 @@ def build(force=False, verbose=False):
             def compile_one(src):
                 obj = os.path.join(od, os.path.basename(src) + ".o")
                 cmd = ([HIPCC, f"--offload-arch={ARCH}"] + [f for f in FLAGS if f != "-shared"] +
-                       [f'-DXS_BUILD_ID="{bid}"', "-c", "-o", obj, src])
+                       [f'-DXS_BUILD_ID="{bid}"', f'-DXS_BUILD_COMPILER="{cc}"', "-c", "-o", obj, src])
                 if verbose:
                     print(" ".join(cmd), file=sys.stderr)
                 subprocess.check_call(cmd)

@@ -120,6 +120,12 @@ const char* xs_version(void) { return "rclone_amd crypt 0.1 (gfx950)"; }
 #endif
 __attribute__((used)) static const char kBuildIdTag[] = "xs-build-id:" XS_BUILD_ID;
 const char* xs_build_id(void) { return kBuildIdTag + 12; }
+// the compiler that built it (sha256 of `hipcc --version`, first 16 hex digits): the loader rebuilds a
+// library whose compiler differs from the one installed next to the tree
+#ifndef XS_BUILD_COMPILER
+#define XS_BUILD_COMPILER "unstamped"
+#endif
+__attribute__((used)) static const char kBuildCompilerTag[] = "xs-build-compiler:" XS_BUILD_COMPILER;
 
 const char* xs_last_error(void) { return g_err.c_str(); }
 

@@ -25,6 +25,14 @@ BLOCK_SIZE = 65552
 DESC = np.dtype([("src", "<u8"), ("dst", "<u8"), ("len", "<u4"), ("res", "<u4"), ("nonce", "u1", (24,))])
 N_COUNTERS = 6  # blocks, bytes, tag failures, round-trip mismatched words, tag digest lo, tag digest hi
 
+# BASELINE configs[3]'s object set, as bench.py's objectset leg and tests/test_objectset_gpu.py
+# both run it: their tag digests are the same number for any world size
+CONFIG3_BLOCKS = 1 << 24  # 1 TiB of 64 KiB blocks
+CONFIG3_KEY = bytes(range(100, 132))
+CONFIG3_NONCE0 = b"\xf0" + b"\xff" * 7 + bytes(range(16))  # the set's nonces carry across byte 8
+CONFIG3_SEED = 0x1417
+CONFIG3_ROUND_BLOCKS = 100_000
+
 
 def _descriptors(nonce0: bytes, gidx: np.ndarray, round_blocks: int, open_mode: bool) -> np.ndarray:
     d = np.zeros(len(gidx), dtype=DESC)

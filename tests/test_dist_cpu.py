@@ -106,6 +106,28 @@ def test_bench_starts_its_own_ranks():
     assert res["config"] == {"ranks_seen": 2, "ranks_reported": 2, "rank_sum": 1, "process_group": "gloo"}
 
 
+def test_bench_starts_eight_ranks():
+    """The driver's N = 8 launch, rehearsed on the CPU: `bench.py --gpus 8 --dry-run` starts eight
+    ranks, they join one gloo group, the counter all-reduce sees all of them, and exactly one line
+    is printed (rank 0's)."""
+    r, lines = _bench(["--gpus", "8", "--dry-run", "--steps", "3"], {"BENCH_DIST_BACKEND": "gloo"}, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout
+    res = lines[0]
+    assert res["n_gpus"] == 8 and res["dry_run"] is True
+    assert res["config"] == {"ranks_seen": 8, "ranks_reported": 8, "rank_sum": sum(range(8)), "process_group": "gloo"}
+
+
+def test_pool_check_timeout_grows_with_devices():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    t = [bench.pool_check_timeout(n) for n in (1, 2, 8)]
+    assert t[0] >= 90 and t[0] < t[1] < t[2] and t[2] >= 200
+
+
 def test_bench_forced_one_rank_group():
     """BENCH_FORCE_PG=1 puts an N = 1 run through a one-rank process group (its own rendezvous on
     127.0.0.1 when no launcher set one): the collectives an N-GPU run makes, on one rank."""

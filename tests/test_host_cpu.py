@@ -87,6 +87,79 @@ def test_stale_library_is_refused(tmp_path):
     assert "REFUSED" in out and "loaded library reports build" in out
 
 
+def test_library_from_another_compiler_is_refused(tmp_path):
+    """The compiler is stamped beside the build id: where hipcc is installed, a library another
+    hipcc / ROCm built counts as stale (rebuilt, or refused with RCLONE_AMD_REBUILD=0)."""
+    from rclone_amd import build
+    if not build.hipcc_available():
+        pytest.skip("no hipcc: the compiler stamp is not checked")
+    data = open(build.LIB, "rb").read()
+    cc = build.compiler_id().encode()
+    i = data.index(build.COMPILER_TAG + cc) + len(build.COMPILER_TAG)
+    other = bytearray(data)
+    other[i:i + 16] = b"0123456789abcdef" if cc != b"0123456789abcdef" else b"fedcba9876543210"
+    out = _probe(tmp_path, bytes(other))
+    assert "REFUSED" in out and "built by compiler" in out
+
+
+_FAKE_HIPCC = r"""#!{py}
+# TEST INFRASTRUCTURE: stands in for hipcc -- --version from the real one, '-c' writes an empty
+# object slowly (widens the race), the link copies the real library and is logged
+import os, shutil, subprocess, sys, time
+args = sys.argv[1:]
+if args == ["--version"]:
+    sys.stdout.write(subprocess.run([{real!r}, "--version"], capture_output=True, text=True).stdout)
+    sys.exit(0)
+out = args[args.index("-o") + 1]
+if "-c" in args:
+    time.sleep(0.5)
+    open(out, "wb").close()
+else:
+    with open({log!r}, "a") as f:
+        f.write("link %d\n" % os.getpid())
+    shutil.copyfile({lib!r}, out)
+"""
+
+
+def test_concurrent_loaders_rebuild_once(tmp_path):
+    """Four processes (ranks of one job) find a stale library at once: exactly one rebuilds it,
+    under the build lock, and all four load the same, current build id.  The package is copied
+    into a scratch tree (same relative paths, hence the same build id), with a stand-in hipcc whose
+    link step hands back this tree's real library."""
+    import shutil
+    import subprocess
+    import sys
+
+    from rclone_amd import build
+    if not build.hipcc_available():
+        pytest.skip("no hipcc")
+    tree = tmp_path / "tree"
+    pkg = tree / "rclone_amd"
+    shutil.copytree(os.path.join(ROOT, "rclone_amd"), pkg,
+                    ignore=shutil.ignore_patterns("__pycache__", "*.so", "*.lock", "*.tmp*"))
+    shutil.copytree(os.path.join(ROOT, "include"), tree / "include")
+    data = bytearray(open(build.LIB, "rb").read())
+    want = build.build_sources_sha256()
+    j = data.index(build.BUILD_ID_TAG + want.encode()) + len(build.BUILD_ID_TAG)
+    data[j:j + 8] = b"00000000" if want[:8] != "00000000" else b"11111111"
+    (pkg / "librclone_crypt.so").write_bytes(bytes(data))  # stale: another build id
+    log = tmp_path / "hipcc.log"
+    fake = tmp_path / "hipcc"
+    fake.write_text(_FAKE_HIPCC.format(py=sys.executable, real=build.HIPCC, log=str(log), lib=build.LIB))
+    fake.chmod(0o755)
+    code = ("import sys; sys.path.insert(0, %r)\nfrom rclone_amd import _lib\nprint('ID', _lib.build_id())" % str(tree))
+    env = dict(os.environ, HIPCC=str(fake), RCLONE_AMD_REBUILD="1")
+    procs = [subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                              env=env, cwd=str(tmp_path)) for _ in range(4)]
+    outs = [p.communicate(timeout=180) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-2000:]
+    ids = {o.split("ID", 1)[1].strip() for o, _ in outs}
+    assert ids == {want}
+    assert log.read_text().count("link") == 1
+    assert build.library_build_id(str(pkg / "librclone_crypt.so")) == want
+
+
 def test_encrypted_decrypted_size(ref_kat):
     for n, e in ref_kat["encrypted_size"]:
         assert crypt.encrypted_size(n) == e

@@ -20,10 +20,12 @@ from rclone_amd.testdata import splitmix64_block
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-TOTAL = int(os.environ.get("RCLONE_AMD_OBJECTSET_BLOCKS", 1 << 24))
-SEED = 0x1417
-KEY = bytes(range(100, 132))
-NONCE0 = b"\xf0" + b"\xff" * 7 + bytes(range(16))  # the set's nonces carry across byte 8
+from rclone_amd.objectset import CONFIG3_BLOCKS, CONFIG3_KEY, CONFIG3_NONCE0, CONFIG3_SEED  # noqa: E402
+
+TOTAL = int(os.environ.get("RCLONE_AMD_OBJECTSET_BLOCKS", CONFIG3_BLOCKS))
+SEED = CONFIG3_SEED
+KEY = CONFIG3_KEY
+NONCE0 = CONFIG3_NONCE0  # the set's nonces carry across byte 8
 
 
 def test_objectset_digest_independent_of_world():
@@ -46,6 +48,8 @@ def test_objectset_digest_independent_of_world():
         blocks, nbytes, fails, mism, d0, d1 = digest_to_u64(tot)
         assert (blocks, nbytes, fails, mism) == (TOTAL, TOTAL * 65536, 0, 0), world
         res[world] = (d0, d1)
+        # the same string bench.py's objectset leg reports (counters.tag_digest)
+        print(f"configs[3] world {world}: {TOTAL} blocks, tag_digest {d1:016x}{d0:016x}")
     assert res[1] == res[2] == res[8]
 
 

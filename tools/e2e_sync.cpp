@@ -20,7 +20,14 @@
 //            encrypter (rc_encrypter_set_md5, host workers; --tee encrypter, the default) or by
 //            the reading thread (--tee reader, crypt.go:516-533's TeeReader as is).
 //            Either way crypt.put then compares the tee hash with the remote's Object.Hash
-//            (CPU MD5 of the stored bytes, cached) unless --check-dst-hash 0.
+//            (CPU MD5 of the stored bytes, cached) unless --check-dst-hash 0.  That check is part of
+//            each put (crypt.go:542-560: Put returns only after o.Hash, memory.go:580-588), so by
+//            default (--put-check inline) it runs inside the transfer, right after the object is
+//            stored: in stream mode on the transfer's own thread, in batch mode on --hash-threads
+//            workers fed as each group lands (other groups' reads and seals go on meanwhile).
+//            sync_GiB_s is the rate with every put's check done; put_only_GiB_s counts to the last
+//            stored object only.  --put-check after runs the checks as a phase after all puts (the
+//            round-4 accounting).
 //   check  : cryptcheck, batch (--check-mode batch, default) -- every local file re-sealed with the
 //            nonce read back from the stored header and MD5'd on the GPU (xs_engine_seal_md5),
 //            compared with the remote's hash; stream (--check-mode stream) -- the unchanged
@@ -38,7 +45,8 @@
 //            and name engines on the same list (RCLONE_AMD_DEVICES): one process over several GPUs.
 //   usage: e2e_sync [--gib G] [--dir D] [--transfers T] [--mode batch|stream]
 //                   [--tee encrypter|reader] [--check-mode batch|stream] [--checkers C]
-//                   [--check-dst-hash 0|1] [--group-mib M] [--lanes L] [--keep]
+//                   [--check-dst-hash 0|1] [--put-check inline|after] [--hash-threads H]
+//                   [--group-mib M] [--lanes L] [--keep]
 //                   [--anchor FILE] [--devices LIST]
 #include <fcntl.h>
 #include <sys/random.h>
@@ -48,6 +56,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -264,9 +274,9 @@ static bool names_batch(rc_cipher* c, int32_t op, const std::vector<const std::s
 int main(int argc, char** argv) {
   double gib = 8.0;
   std::string dir = "/tmp/rc_e2e_src", mode = "batch";
-  int transfers = 16, check_dst = 1, keep = 0, nlanes = 4, checkers = 8;
+  int transfers = 16, check_dst = 1, keep = 0, nlanes = 4, checkers = 8, hash_threads = 0;
   uint64_t group_mib = 4096;
-  std::string anchor, devices, tee_mode = "encrypter", check_mode = "batch";
+  std::string anchor, devices, tee_mode = "encrypter", check_mode = "batch", put_check = "inline";
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
     auto nx = [&] { return std::string(i + 1 < argc ? argv[++i] : ""); };
@@ -283,6 +293,8 @@ int main(int argc, char** argv) {
     else if (a == "--tee") tee_mode = nx();
     else if (a == "--check-mode") check_mode = nx();
     else if (a == "--checkers") checkers = std::max(1, atoi(nx().c_str()));
+    else if (a == "--put-check") put_check = nx();
+    else if (a == "--hash-threads") hash_threads = std::max(1, atoi(nx().c_str()));
     else {
       fprintf(stderr, "unknown argument %s\n", a.c_str());
       return 2;
@@ -291,6 +303,9 @@ int main(int argc, char** argv) {
   if (mode != "batch" && mode != "stream") return 2;
   if (tee_mode != "encrypter" && tee_mode != "reader") return 2;
   if (check_mode != "batch" && check_mode != "stream") return 2;
+  if (put_check != "inline" && put_check != "after") return 2;
+  if (!hash_threads) hash_threads = transfers;
+  const bool inline_check = check_dst && put_check == "inline";
   std::vector<int> devs;
   if (!devices.empty()) {
     setenv("RCLONE_AMD_DEVICES", devices.c_str(), 1);  // rc_* handles and name engines
@@ -439,7 +454,14 @@ int main(int argc, char** argv) {
   };
   // ---- sync
   double t_sync = 0, t_dst = 0, sync_read = 0, sync_gpu = 0, t_names_enc = 0, t_names_dec = 0;
+  double t_puts = 0;  // to the last stored object (put's own hash checks not awaited)
   uint64_t put_mismatch = 0, name_mismatch = 0;
+  std::atomic<uint64_t> bad_put{0};
+  // crypt.put's tail (crypt.go:542-560): the remote's MD5 of what it stored vs the tee hash
+  auto put_check_one = [&](size_t i) {
+    dst_hash(objs[i]);
+    if (memcmp(objs[i].tee, objs[i].dst, 16)) bad_put++;
+  };
   const double tn0 = now();
   {  // crypt.Put's remote name: EncryptFileName(rel) for the whole listing (crypt.go:517)
     std::vector<const std::string*> in(objs.size());
@@ -451,6 +473,27 @@ int main(int argc, char** argv) {
   t_names_enc = now() - tn0;
   if (mode == "batch") {
     const double t0 = now();
+    // inline put checks: workers take each object as soon as its group is stored
+    std::mutex qmu;
+    std::condition_variable qcv;
+    std::deque<size_t> q;
+    bool closing = false;
+    std::vector<std::thread> hashers;
+    if (inline_check)
+      for (int t = 0; t < hash_threads; t++)
+        hashers.emplace_back([&] {
+          for (;;) {
+            size_t i;
+            {
+              std::unique_lock<std::mutex> lk(qmu);
+              qcv.wait(lk, [&] { return closing || !q.empty(); });
+              if (q.empty()) return;
+              i = q.front();
+              q.pop_front();
+            }
+            put_check_one(i);
+          }
+        });
     run_groups([&](int l, size_t g, const std::vector<uint64_t>& offs) {
       const size_t a = groups[g].first, n = groups[g].second - a;
       std::vector<uint8_t> md5(16 * n);
@@ -461,7 +504,21 @@ int main(int argc, char** argv) {
         return;
       }
       for (size_t k = 0; k < n; k++) memcpy(objs[a + k].tee, md5.data() + 16 * k, 16);
+      if (inline_check) {
+        {
+          std::lock_guard<std::mutex> lk(qmu);
+          for (size_t k = 0; k < n; k++) q.push_back(a + k);
+        }
+        qcv.notify_all();
+      }
     });
+    t_puts = now() - t0 + t_names_enc;
+    {
+      std::lock_guard<std::mutex> lk(qmu);
+      closing = true;
+    }
+    qcv.notify_all();
+    for (auto& t : hashers) t.join();
     t_sync = now() - t0 + t_names_enc;
     sync_read = t_read;
     sync_gpu = t_gpu;
@@ -511,20 +568,20 @@ int main(int argc, char** argv) {
         failures++;
         return;
       }
+      if (inline_check) put_check_one(i);  // the same transfer, before Put returns
     });
     t_sync = now() - t0 + t_names_enc;
+    t_puts = t_sync;
   }
-  if (check_dst) {  // crypt.put: srcHash (tee) vs dstHash (the remote's MD5 of what it stored)
+  if (check_dst && !inline_check) {  // --put-check after: the checks as a phase of their own
     const double t0 = now();
-    std::atomic<uint64_t> bad{0};
-    parallel_for(objs.size(), transfers, [&](size_t i) {
-      dst_hash(objs[i]);
-      if (memcmp(objs[i].tee, objs[i].dst, 16)) bad++;
-    });
+    parallel_for(objs.size(), transfers, put_check_one);
     t_dst = now() - t0;
-    fprintf(stderr, "e2e: sync %.1f s, destination hash %.1f s\n", t_sync, t_dst);
-    put_mismatch = bad;
+    t_puts = t_sync;
+    t_sync += t_dst;
   }
+  if (check_dst) fprintf(stderr, "e2e: sync %.1f s with put checks (%s), puts alone %.1f s\n", t_sync, put_check.c_str(), t_puts);
+  put_mismatch = bad_put;
   // ---- cryptcheck: re-seal each local file with the stored nonce, MD5 on the GPU, compare
   auto cryptcheck = [&](std::vector<uint8_t>& differ) {
     differ.assign(objs.size(), 0);
@@ -662,15 +719,16 @@ int main(int argc, char** argv) {
   printf("{\"config\": \"configs[4] e2e: sync local tree -> crypt(memory), cryptcheck\", \"mode\": \"%s\", "
          "\"tee\": \"%s\", \"check_mode\": \"%s\", \"checkers\": %d, "
          "\"objects\": %zu, \"gib\": %.3f, \"transfers\": %d, \"lanes\": %d, \"group_mib\": %llu, "
-         "\"sync_s\": %.3f, \"sync_GiB_s\": %.2f, \"dst_hash_s\": %.3f, \"sync_with_hash_check_GiB_s\": %.2f, "
+         "\"put_check\": \"%s\", \"hash_threads\": %d, "
+         "\"sync_s\": %.3f, \"sync_GiB_s\": %.2f, \"put_only_s\": %.3f, \"put_only_GiB_s\": %.2f, \"dst_hash_phase_s\": %.3f, "
          "\"cryptcheck_s\": %.3f, \"cryptcheck_GiB_s\": %.2f, \"put_hash_mismatches\": %llu, "
          "\"cryptcheck_differences\": %llu, \"verified_objects\": %llu, \"verify_failures\": %llu, "
          "\"corruption_flagged\": %llu, \"names_encrypt_s\": %.4f, \"names_decrypt_s\": %.4f, "
          "\"name_mismatches\": %llu, \"example_remote_name\": \"%s\", "
          "\"anchored_objects\": %llu, \"devices\": \"%s\", \"tree_write_s\": %.2f, \"lane_seconds\": {\"sync_read\": %.3f, "
          "\"sync_gpu\": %.3f, \"check_read\": %.3f, \"check_gpu\": %.3f}, \"ok\": %s}\n",
-         mode.c_str(), mode == "stream" ? tee_mode.c_str() : "gpu", check_mode.c_str(), checkers, objs.size(), g, transfers, lanes, (unsigned long long)group_mib, t_sync, g / t_sync, t_dst,
-         check_dst ? g / (t_sync + t_dst) : 0.0, t_check, g / t_check, (unsigned long long)put_mismatch,
+         mode.c_str(), mode == "stream" ? tee_mode.c_str() : "gpu", check_mode.c_str(), checkers, objs.size(), g, transfers, lanes, (unsigned long long)group_mib,
+         check_dst ? put_check.c_str() : "off", hash_threads, t_sync, g / t_sync, t_puts, g / t_puts, t_dst, t_check, g / t_check, (unsigned long long)put_mismatch,
          (unsigned long long)ndiff, (unsigned long long)verified, (unsigned long long)verify_bad,
          (unsigned long long)flagged, t_names_enc, t_names_dec, (unsigned long long)name_mismatch,
          objs.empty() ? "" : objs.back().remote.c_str(), (unsigned long long)anchored, devices.c_str(), t_gen, sync_read, sync_gpu, check_read, check_gpu, ok ? "true" : "false");
