@@ -443,7 +443,7 @@ def objectset_leg(args, world, rank, dev, dist):
     import torch
 
     from rclone_amd.objectset import (CONFIG3_BLOCKS, CONFIG3_KEY, CONFIG3_NONCE0, CONFIG3_ROUND_BLOCKS,
-                                      CONFIG3_SEED, RankRunner, digest_to_u64)
+                                      CONFIG3_SEED, CONFIG3_TAG_DIGEST, RankRunner, digest_to_u64)
     total = int(os.environ.get("BENCH_OBJECTSET_BLOCKS", CONFIG3_BLOCKS))
     t_setup = time.perf_counter()
     r = RankRunner(CONFIG3_KEY, CONFIG3_NONCE0, total, world, rank, CONFIG3_ROUND_BLOCKS, CONFIG3_SEED, dev)
@@ -454,7 +454,9 @@ def objectset_leg(args, world, rank, dev, dist):
             r.run_all()
     el, counters, seal_ms, open_ms = time_objectset(r, args.objectset_steps, warm, world, dev, dist)
     blocks, nbytes, fails, mism, d0, d1 = digest_to_u64(counters)
-    ok = fails == 0 and mism == 0 and blocks == args.objectset_steps * total
+    digest = f"{d1:016x}{d0:016x}"  # the last pass's, summed over the ranks
+    full = total == CONFIG3_BLOCKS
+    ok = fails == 0 and mism == 0 and blocks == args.objectset_steps * total and (digest == CONFIG3_TAG_DIGEST or not full)
     del r
     torch.cuda.empty_cache()
     if rank != 0:
@@ -469,7 +471,10 @@ def objectset_leg(args, world, rank, dev, dist):
             "open_kernel_ms_avg": round(sum(open_ms) / max(len(open_ms), 1), 4),
             "setup_s": round(setup_s, 2),
             "counters": {"blocks": blocks, "bytes": nbytes, "tag_failures": fails, "roundtrip_mismatch_words": mism,
-                         "tag_digest": f"{d1:016x}{d0:016x}"}}
+                         "tag_digest": digest,
+                         "tag_digest_expected": CONFIG3_TAG_DIGEST if full else None,
+                         "digest_source": "one pass, summed over ranks; expected = tests/test_objectset_gpu.py at world "
+                                          "1/2/8 (rclone_amd.objectset.CONFIG3_TAG_DIGEST)"}}
 
 
 def run_objectset(args, world, rank, dev, dist):

@@ -82,8 +82,5 @@ hipError_t launch_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t f
 
 void set_error(const char* fmt, ...);
 std::vector<int> default_devices();  // see rc_internal.h
-#ifdef XS_CLOCK_PROBE
-void probe_read(unsigned long long* host, size_t n);
-#endif
 
 }  // namespace xs

@@ -34,22 +34,14 @@
 #include "xs_internal.h"
 #include "xs_salsa_lazy.h"
 
+// Tuning parameters (launch thresholds and occupancy targets; runtime env overrides where
+// noted).  Designs that measured slower (double-buffered staging, permlane output transpose,
+// XCD-remapped workgroup order, VALU data XOR, VALU Poly1305 for full blocks, the one- and
+// four-crypt-wave fused kernels) are not in this file: DESIGN.md section 3 records their A/Bs.
 // XS_SEAL_WPE / XS_OPEN_WPE: minimum waves per SIMD the register allocator must allow
 // (amdgpu_waves_per_eu) for the seal / open kernels.
-#ifndef XS_SALSA_LAZY  // Salsa20 double rounds with deferred XORs (v_xad_u32 / v_bitop3_b32)
-#define XS_SALSA_LAZY 1
-#endif
-#ifndef XS_ST_PERM  // output transpose with v_permlane{32,16}_swap instead of the LDS round trip
-#define XS_ST_PERM 0
-#endif
-#ifndef XS_DBUF  // double-buffered staging (8 KiB per wave)
-#define XS_DBUF 0
-#endif
 #ifndef XS_FUSED_MAX  // single-request descriptor batches up to this many blocks: keygen + crypt in one launch
 #define XS_FUSED_MAX 16
-#endif
-#ifndef XS_FUSED_V  // fused kernel: 1 = keygen then split crypt, 2 / 3 = key schedule overlapped with the
-#define XS_FUSED_V 3  // keystream, four / eight crypt waves
 #endif
 #ifndef XS_KEYGEN_WIDE_MAX  // batches up to this many blocks get one keygen wave per block (latency)
 #define XS_KEYGEN_WIDE_MAX 16
@@ -57,17 +49,11 @@
 #ifndef XS_SPLIT_MAX  // batches up to this many blocks run four waves per block (latency)
 #define XS_SPLIT_MAX 256
 #endif
-#ifndef XS_XCD_REMAP
-#define XS_XCD_REMAP 0
-#endif
 #ifndef XS_SEAL_WPE  // 5 waves per SIMD (<= 96 VGPRs): hides the LDS atomics' latency; paired
 #define XS_SEAL_WPE 5  // -0.7% seal / -1.1% open against 4
 #endif
 #ifndef XS_OPEN_WPE
 #define XS_OPEN_WPE 5
-#endif
-#ifndef XS_LDS_XOR  // data XOR keystream and the MFMA operand's sign bias by LDS atomics on the staged
-#define XS_LDS_XOR 1  // words (1), or on the VALU (0)
 #endif
 
 
@@ -124,14 +110,13 @@ __device__ __forceinline__ void salsa_rounds_lazy(uint32_t (&x)[16]) {
   for (int i = 0; i < 16; i++)
     if ((XS_LAZY_MASK >> i) & 1u) x[i] ^= t[i];
 }
-__device__ __forceinline__ void salsa_rounds9(uint32_t (&x)[16]) { salsa_rounds_n(x, 9); }
 
 constexpr uint32_t SIG0 = 0x61707865u, SIG1 = 0x3320646eu, SIG2 = 0x79622d32u, SIG3 = 0x6b206574u;
 
 // A wave-uniform value handed to the compiler as lane-varying: the computation that follows runs
 // on the VALU instead of the scalar unit.  For a latency-bound single state (HSalsa20 of a ranged
 // read's block) the SALU is ~3x slower: no one-instruction rotate, one scalar op in flight per
-// wave (measured 6.8 us vs ~2 us for the 20 rounds, tools/fused_probe.cpp).
+// wave (measured 6.8 us vs ~2 us for the 20 rounds with phase marks, round 2).
 __device__ __forceinline__ uint32_t as_varying(uint32_t x) {
   uint32_t v;
   asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "v"(x));
@@ -238,7 +223,6 @@ __device__ __forceinline__ void salsa20_block_pre(const SalsaPre& p, uint32_t ct
   x[13] = p.x13 ^ rotl(x[12] + p.x15, 9);
   x[14] = p.x14 ^ rotl(x[13] + x[12], 13);
   x[15] = p.x15 ^ rotl(x[14] + x[13], 18);
-#if XS_SALSA_LAZY
   // double rounds 2..10 with deferred XORs (xs_salsa_lazy.h): word i is b[i] ^ t[i] when bit
   // i of XS_LAZY_MASK is set, else b[i]; the feed-forward absorbs the pending XOR (v_xad_u32)
   uint32_t t[16];
@@ -252,25 +236,6 @@ __device__ __forceinline__ void salsa20_block_pre(const SalsaPre& p, uint32_t ct
     if ((XS_LAZY_MASK >> i) & 1u) out[i] = xs_xad(x[i], t[i], in[i]);
     else out[i] = x[i] + in[i];
   }
-  return;
-#endif
-  salsa_rounds9(x);
-  out[0] = x[0] + SIG0;
-  out[1] = x[1] + p.k[0];
-  out[2] = x[2] + p.k[1];
-  out[3] = x[3] + p.k[2];
-  out[4] = x[4] + p.k[3];
-  out[5] = x[5] + SIG1;
-  out[6] = x[6] + p.n0;
-  out[7] = x[7] + p.n1;
-  out[8] = x[8] + ctr;
-  out[9] = x[9];
-  out[10] = x[10] + SIG2;
-  out[11] = x[11] + p.k[4];
-  out[12] = x[12] + p.k[5];
-  out[13] = x[13] + p.k[6];
-  out[14] = x[14] + p.k[7];
-  out[15] = x[15] + SIG3;
 }
 
 // ---------------------------------------------------------------- Poly1305, radix 2^26
@@ -361,72 +326,10 @@ __device__ __forceinline__ void padd_part(P5& h, uint32_t w0, uint32_t w1, uint3
   h.v[4] += (w3 >> 8);
 }
 
-// ---------------------------------------------------------------- Poly1305, radix 2^32
-// For multiplications by the clamped key r itself (r1..r3 divisible by 4, all words < 2^28)
-// the 32-bit-word form needs 20 multiply-adds and no limb splitting (OpenSSL's 32-bit
-// poly1305_blocks): h = (h + c + 2^128) * r, partially reduced (h4 <= 4 on exit).
+// ---------------------------------------------------------------- Poly1305, radix 2^32 words
 struct P32 {
   uint32_t w0, w1, w2, w3, w4;
 };
-struct RClamp {
-  uint32_t r0, r1, r2, r3, s1, s2, s3;  // s_i = r_i + r_i/4 = 5 r_i / 4
-};
-
-__device__ __forceinline__ void pstep32(P32& h, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, const RClamp& r) {
-  // h += c + 2^128 (32-bit add-with-carry chain)
-  unsigned cy;
-  const uint32_t h0 = __builtin_addc(h.w0, c0, 0u, &cy);
-  const uint32_t h1 = __builtin_addc(h.w1, c1, cy, &cy);
-  const uint32_t h2 = __builtin_addc(h.w2, c2, cy, &cy);
-  const uint32_t h3 = __builtin_addc(h.w3, c3, cy, &cy);
-  const uint32_t h4 = __builtin_addc(h.w4, 1u, cy, &cy);
-  // column sums (v_mad_u64_u32 chains)
-  const uint64_t d0 = (uint64_t)h0 * r.r0 + (uint64_t)h1 * r.s3 + (uint64_t)h2 * r.s2 + (uint64_t)h3 * r.s1;
-  const uint64_t d1 = (uint64_t)h0 * r.r1 + (uint64_t)h1 * r.r0 + (uint64_t)h2 * r.s3 + (uint64_t)h3 * r.s2 +
-                      (uint64_t)h4 * r.s1;
-  const uint64_t d2 = (uint64_t)h0 * r.r2 + (uint64_t)h1 * r.r1 + (uint64_t)h2 * r.r0 + (uint64_t)h3 * r.s3 +
-                      (uint64_t)h4 * r.s2;
-  const uint64_t d3 = (uint64_t)h0 * r.r3 + (uint64_t)h1 * r.r2 + (uint64_t)h2 * r.r1 + (uint64_t)h3 * r.r0 +
-                      (uint64_t)h4 * r.s3;
-  // carry the high words up: d_{i+1} += d_i >> 32
-  uint32_t l0 = (uint32_t)d0, l1 = (uint32_t)d1, l2 = (uint32_t)d2, l3 = (uint32_t)d3;
-  uint32_t u1 = (uint32_t)(d1 >> 32), u2 = (uint32_t)(d2 >> 32), u3 = (uint32_t)(d3 >> 32);
-  l1 = __builtin_addc(l1, (uint32_t)(d0 >> 32), 0u, &cy);
-  u1 = u1 + cy;
-  l2 = __builtin_addc(l2, u1, 0u, &cy);
-  u2 = u2 + cy;
-  l3 = __builtin_addc(l3, u2, 0u, &cy);
-  u3 = u3 + cy;
-  const uint32_t h4n = h4 * r.r0 + u3;
-  // fold bits >= 130: h += (h4n >> 2) * 5
-  const uint32_t c = (h4n >> 2) + (h4n & ~3u);
-  h.w0 = __builtin_addc(l0, c, 0u, &cy);
-  h.w1 = __builtin_addc(l1, 0u, cy, &cy);
-  h.w2 = __builtin_addc(l2, 0u, cy, &cy);
-  h.w3 = __builtin_addc(l3, 0u, cy, &cy);
-  h.w4 = (h4n & 3u) + cy;
-}
-
-// h += c + 2^128 in radix 2^32 (no multiply)
-__device__ __forceinline__ void padd32(P32& h, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
-  unsigned cy;
-  h.w0 = __builtin_addc(h.w0, c0, 0u, &cy);
-  h.w1 = __builtin_addc(h.w1, c1, cy, &cy);
-  h.w2 = __builtin_addc(h.w2, c2, cy, &cy);
-  h.w3 = __builtin_addc(h.w3, c3, cy, &cy);
-  h.w4 = h.w4 + 1u + cy;
-}
-
-// radix 2^32 (w4 < 2^6) -> radix 2^26 limbs (limb 4 < 2^27), exact
-__device__ __forceinline__ P5 to26(const P32& h) {
-  P5 o;
-  o.v[0] = h.w0 & M26;
-  o.v[1] = alignbit(h.w1, h.w0, 26) & M26;
-  o.v[2] = alignbit(h.w2, h.w1, 20) & M26;
-  o.v[3] = alignbit(h.w3, h.w2, 14) & M26;
-  o.v[4] = alignbit(h.w4, h.w3, 8);
-  return o;
-}
 
 // radix 2^26 limbs (each < 2^27) -> radix 2^32, exact (additive repacking with carries)
 __device__ __forceinline__ P32 to32(const P5& o) {
@@ -779,20 +682,6 @@ __global__ void __launch_bounds__(64) xs_keygen(KeyArg key, NonceArg nonce0, uin
 // is canonical, so tags and ciphertext equal the narrow keygen's.
 // The body: one wave (lanes l = threadIdx.x & 63) builds block b's key schedule into *o (global
 // memory, or LDS in the fused kernels).
-#ifdef XS_F2_PROBE
-extern __device__ unsigned long long xs_f2_probe[2 * 10 * 16];
-#define KG_MARK(slot)                                                                              \
-  do {                                                                                             \
-    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
-    const unsigned long long c_ = __builtin_amdgcn_s_memtime();                                    \
-    if (blockIdx.x == 0 && (threadIdx.x >> 6) == (blockDim.x >> 6) - 1u && l < 2u)                   \
-      xs_f2_probe[160 * l + 16 * 9 + (slot)] = l ? c_ : t_;                                          \
-  } while (0)
-#else
-#define KG_MARK(slot) \
-  do {                \
-  } while (0)
-#endif
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // Wait until another wave of the workgroup raised *flag (LDS), then read the 8-word subkey it
@@ -865,7 +754,6 @@ __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32
                                                  const uint32_t* sk_flag, const Mid& mid, uint32_t* cd_flag) {
   const uint32_t l = threadIdx.x & 63u;
   uint32_t sk[8];
-  KG_MARK(0);
   if (sk_lds) {
     lds_wait_subkey(sk_flag, sk_lds, sk);
   } else {
@@ -877,10 +765,8 @@ __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32
     sk[0] = x[0]; sk[1] = x[5]; sk[2] = x[10]; sk[3] = x[15];
     sk[4] = x[6]; sk[5] = x[7]; sk[6] = x[8]; sk[7] = x[9];
   }
-  KG_MARK(1);
   uint32_t ks[16];
   salsa20_block_lazy(sk, n[4], n[5], l < 32 ? 0u : 1024u, ks);
-  KG_MARK(2);
   if (l == 32 && len > XS_BLOCK_DATA - 32) {
 #pragma unroll
     for (int i = 0; i < 8; i++) o->ks1024[i] = ks[i];
@@ -964,7 +850,6 @@ __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32
         const P5 q = pmul(a, c);
         if (act || own) p = q;
       }
-      KG_MARK(3 + m);
       if (m == 1) {  // C[b] = lane b, D[a] = lane 9 + a are final: out now (cd_flag: LDS, raised after)
         if (l < 8) put5(o->full.C[l], p);
         else if (l >= 9 && l < 18) put5(o->full.D[l - 9], p);
@@ -998,7 +883,6 @@ __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32
       const P5 q = pmul(a, p);
       if (l >= kLaneE && l <= kLaneKlo) p = q;
     }
-    KG_MARK(7);
     P5 e, bq, k;
 #pragma unroll
     for (int i = 0; i < 5; i++) {
@@ -1009,7 +893,6 @@ __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32
     // pmul outputs (limbs < 2^26 + 2^6) are valid subtrahends for psub; corr is canonical, the
     // same value full_corr gives
     const P5 cr = pcanon(psub(psub(e, bq), k));
-    KG_MARK(9);
     if (l == 0) put5(o->corr, cr);
     return;
   }
@@ -1048,18 +931,10 @@ __global__ void __launch_bounds__(64) xs_keygen_wide(KeyArg key, NonceArg nonce0
 // keystream is ready, XORed and stored.  Lane 63 also owns chunks 4094, 4095 (keystream block
 // 1024, precomputed by keygen), so every lane's Horner multipliers are uniform: r inside a
 // group, r^253 between groups.
-#ifndef XS_POLY_MFMA
-#define XS_POLY_MFMA 1  // full-block Poly1305 on the matrix cores
-#endif
-#if !XS_POLY_MFMA
-#error "full blocks need the matrix-core path: keygen writes no T1/T2 tables for them"
-#endif
-#if XS_POLY_MFMA
-constexpr int STAGE_WORDS = XS_DBUF ? 2048 : 1024;
-constexpr int WAVE_LDS_WORDS = STAGE_WORDS + 768;  // 4 KiB staging (x2 with XS_DBUF) + 3 KiB Toeplitz table
-#else
-constexpr int WAVE_LDS_WORDS = 1024;
-#endif
+// Full blocks run Poly1305 on the matrix cores (crypt_block_mfma); crypt_block below is the
+// partial-block path (VALU Horner).
+constexpr int STAGE_WORDS = 1024;
+constexpr int WAVE_LDS_WORDS = STAGE_WORDS + 768;  // 4 KiB staging + 3 KiB Toeplitz table
 constexpr int LDS_WORDS = 4 * WAVE_LDS_WORDS;
 constexpr uint32_t LANES = 64, GROUPS = 16;
 typedef __attribute__((address_space(3))) void lds_void;
@@ -1069,12 +944,14 @@ __device__ __forceinline__ uint32_t keep_mask(uint32_t L, uint32_t i) {
   return (L >= 4u * i + 4u) ? 0xffffffffu : (L <= 4u * i ? 0u : ((1u << (8u * (L - 4u * i))) - 1u));
 }
 
-template <bool SEAL, bool FULL>
+// A partial block (n < 65536 bytes): VALU Horner per lane over its chunks, uniform multipliers
+// r inside a group and r^253 between groups, final r^e from the key schedule's T1/T2 tables.
+template <bool SEAL>
 __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, const uint8_t* __restrict__ pin,
                                             uint8_t* __restrict__ pout, uint32_t n, uint32_t* wb, P5& h) {
   const uint32_t l = threadIdx.x & 63u;
-  const int nc = FULL ? 4096 : (int)((n + 15u) >> 4);
-  const int nfull = FULL ? 4096 : (int)(n >> 4);  // chunks that are whole 16-byte chunks
+  const int nc = (int)((n + 15u) >> 4);
+  const int nfull = (int)(n >> 4);  // chunks that are whole 16-byte chunks
   uint32_t k[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) k[i] = bk->subkey[i];
@@ -1086,13 +963,6 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
     RR.v[i] = bk->R[i];
   }
   const PMul Mr = pmul_prep(rr), MR = pmul_prep(RR);
-  RClamp rc;
-  {
-    const P32 r32 = to32(rr);
-    rc.r0 = r32.w0; rc.r1 = r32.w1; rc.r2 = r32.w2; rc.r3 = r32.w3;
-    rc.s1 = rc.r1 + (rc.r1 >> 2); rc.s2 = rc.r2 + (rc.r2 >> 2); rc.s3 = rc.r3 + (rc.r3 >> 2);
-  }
-  P32 h32 = {0, 0, 0, 0, 0};  // FULL path accumulator (radix 2^32)
   int c_last = -1;
   P5 t1, t2;
 
@@ -1100,22 +970,13 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
   for (int s = 0; s < (int)GROUPS; s++) {
     const uint32_t K = l + LANES * (uint32_t)s;
     const int cfirst = 4 * (int)K - 2;
-    if (!FULL && cfirst >= nc) break;
+    if (cfirst >= nc) break;
     // stage this group's input (whole chunks only) into the wave's LDS slot
     const uint8_t* src = pin + 64u * K - 32u;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const int c = cfirst + j;
-      const bool whole = FULL ? (c >= 0) : (c >= 0 && c < nfull);
-      if (whole) __builtin_amdgcn_global_load_lds(src + 16 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
-    }
-    if (FULL && s == (int)GROUPS - 1) {  // final-exponent tables, needed after the loop
-      const uint32_t e = (l == 63u) ? 0u : 254u - 4u * l;
-#pragma unroll
-      for (int i = 0; i < 5; i++) {
-        t1.v[i] = bk->part.T1[e & 31u][i];
-        t2.v[i] = bk->part.T2[e >> 5][i];
-      }
+      if (c >= 0 && c < nfull) __builtin_amdgcn_global_load_lds(src + 16 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
     }
     uint32_t ks[16];
     salsa20_block_pre(pre, K, ks);
@@ -1130,50 +991,37 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const int c = cfirst + j;
-      if (FULL) {
-        plen[j] = 16u;
-        (void)c;
-      } else {
-        plen[j] = (c < 0 || c >= nc) ? 0u : ((c < nfull) ? 16u : (n & 15u));
+      plen[j] = (c < 0 || c >= nc) ? 0u : ((c < nfull) ? 16u : (n & 15u));
+    }
+    // the block's last chunk may be partial: byte loads by its owner
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (plen[j] != 0u && plen[j] != 16u) {
+        const uint32_t off = 16u * (uint32_t)(cfirst + j);
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint32_t i = 0; i < plen[j]; i++) w[i >> 2] |= (uint32_t)pin[off + i] << (8u * (i & 3u));
+        d[4 * j] = w[0]; d[4 * j + 1] = w[1]; d[4 * j + 2] = w[2]; d[4 * j + 3] = w[3];
       }
     }
-    if (!FULL) {
-      // the block's last chunk may be partial: byte loads by its owner
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        if (plen[j] != 0u && plen[j] != 16u) {
-          const uint32_t off = 16u * (uint32_t)(cfirst + j);
-          uint32_t w[4] = {0, 0, 0, 0};
-          for (uint32_t i = 0; i < plen[j]; i++) w[i >> 2] |= (uint32_t)pin[off + i] << (8u * (i & 3u));
-          d[4 * j] = w[0]; d[4 * j + 1] = w[1]; d[4 * j + 2] = w[2]; d[4 * j + 3] = w[3];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        if (plen[j] == 0u) { d[4 * j] = 0; d[4 * j + 1] = 0; d[4 * j + 2] = 0; d[4 * j + 3] = 0; }
-      }
+    for (int j = 0; j < 4; j++) {
+      if (plen[j] == 0u) { d[4 * j] = 0; d[4 * j + 1] = 0; d[4 * j + 2] = 0; d[4 * j + 3] = 0; }
     }
     uint32_t o[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) o[i] = d[i] ^ ks[i];
-    if (!FULL) {
 #pragma unroll
-      for (int j = 0; j < 4; j++) {  // absent chunks hash as zero; partial chunks keep L bytes
-        if (plen[j] == 0u) { o[4 * j] = 0; o[4 * j + 1] = 0; o[4 * j + 2] = 0; o[4 * j + 3] = 0; }
-        if (plen[j] != 16u) {
+    for (int j = 0; j < 4; j++) {  // absent chunks hash as zero; partial chunks keep L bytes
+      if (plen[j] == 0u) { o[4 * j] = 0; o[4 * j + 1] = 0; o[4 * j + 2] = 0; o[4 * j + 3] = 0; }
+      if (plen[j] != 16u) {
 #pragma unroll
-          for (int i = 0; i < 4; i++) o[4 * j + i] &= keep_mask(plen[j], (uint32_t)i);
-        }
+        for (int i = 0; i < 4; i++) o[4 * j + i] &= keep_mask(plen[j], (uint32_t)i);
       }
     }
     uint8_t* dst = pout + 64u * K - 32u;
-    const bool key_slots = FULL && s == 0 && l == 0u;  // chunks -2, -1 of K = 0: the Poly1305 key
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      if (FULL) {
-        if (j >= 2 || !key_slots)
-          *reinterpret_cast<uint4*>(dst + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
-      } else if (plen[j] == 16u) {
+      if (plen[j] == 16u) {
         *reinterpret_cast<uint4*>(dst + 16 * j) = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
       } else if (plen[j] != 0u) {
         for (uint32_t i = 0; i < plen[j]; i++) dst[16 * j + i] = (uint8_t)(o[4 * j + (i >> 2)] >> (8u * (i & 3u)));
@@ -1183,47 +1031,34 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
     const uint32_t* cw = SEAL ? o : d;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      if (FULL) {
-        if (j < 3 || s == (int)GROUPS - 1) {
-          pstep32(h32, cw[4 * j], cw[4 * j + 1], cw[4 * j + 2], cw[4 * j + 3], rc);
-        } else {  // gap to the lane's next group: * r^253 in radix 2^26
-          padd32(h32, cw[4 * j], cw[4 * j + 1], cw[4 * j + 2], cw[4 * j + 3]);
-          h32 = to32(pmul_u(to26(h32), MR));
+      if (plen[j] != 0u) {
+        uint32_t w0 = cw[4 * j], w1 = cw[4 * j + 1], w2 = cw[4 * j + 2], w3 = cw[4 * j + 3];
+        uint32_t pad = 1u << 24;
+        if (plen[j] != 16u) {  // 0x01 after the last byte, no 2^128 bit
+          const uint32_t L = plen[j];
+          const uint32_t bit = 1u << (8u * (L & 3u));
+          w0 |= (L >> 2) == 0u ? bit : 0u;
+          w1 |= (L >> 2) == 1u ? bit : 0u;
+          w2 |= (L >> 2) == 2u ? bit : 0u;
+          w3 |= (L >> 2) == 3u ? bit : 0u;
+          pad = 0u;
         }
-        if (j == 1 && key_slots) {  // discard what lane 0 hashed for the key slots
-          h32.w0 = h32.w1 = h32.w2 = h32.w3 = h32.w4 = 0;
-        }
-      } else {
-        if (plen[j] != 0u) {
-          uint32_t w0 = cw[4 * j], w1 = cw[4 * j + 1], w2 = cw[4 * j + 2], w3 = cw[4 * j + 3];
-          uint32_t pad = 1u << 24;
-          if (plen[j] != 16u) {  // 0x01 after the last byte, no 2^128 bit
-            const uint32_t L = plen[j];
-            const uint32_t bit = 1u << (8u * (L & 3u));
-            w0 |= (L >> 2) == 0u ? bit : 0u;
-            w1 |= (L >> 2) == 1u ? bit : 0u;
-            w2 |= (L >> 2) == 2u ? bit : 0u;
-            w3 |= (L >> 2) == 3u ? bit : 0u;
-            pad = 0u;
-          }
-          h.v[0] += w0 & M26;
-          h.v[1] += alignbit(w1, w0, 26) & M26;
-          h.v[2] += alignbit(w2, w1, 20) & M26;
-          h.v[3] += alignbit(w3, w2, 14) & M26;
-          h.v[4] += (w3 >> 8) | pad;
-          const bool use_R = (j == 3) && (s < (int)GROUPS - 1) && (cfirst + 4 * (int)LANES < nc);
-          PMul M;
+        h.v[0] += w0 & M26;
+        h.v[1] += alignbit(w1, w0, 26) & M26;
+        h.v[2] += alignbit(w2, w1, 20) & M26;
+        h.v[3] += alignbit(w3, w2, 14) & M26;
+        h.v[4] += (w3 >> 8) | pad;
+        const bool use_R = (j == 3) && (s < (int)GROUPS - 1) && (cfirst + 4 * (int)LANES < nc);
+        PMul M;
 #pragma unroll
-          for (int i = 0; i < 5; i++) {
-            M.m[i] = use_R ? MR.m[i] : Mr.m[i];
-            M.s[i] = use_R ? MR.s[i] : Mr.s[i];
-          }
-          h = pmul_u(h, M);
-          c_last = cfirst + j;
+        for (int i = 0; i < 5; i++) {
+          M.m[i] = use_R ? MR.m[i] : Mr.m[i];
+          M.s[i] = use_R ? MR.s[i] : Mr.s[i];
         }
+        h = pmul_u(h, M);
+        c_last = cfirst + j;
       }
     }
-    if (FULL) c_last = cfirst + 3;
   }
   // lane 63 owns chunks 4094, 4095 (keystream block 1024 words 0..7)
   if (l == 63u && nc > 4094) {
@@ -1232,7 +1067,7 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
       const int c = 4094 + j;
       if (c >= nc) break;
       const uint32_t off = 16u * (uint32_t)c;
-      const uint32_t L = FULL ? 16u : ((n - off) < 16u ? (n - off) : 16u);
+      const uint32_t L = (n - off) < 16u ? (n - off) : 16u;
       uint32_t w[4], o4[4];
       if (L == 16u) {
         const uint4 v = *reinterpret_cast<const uint4*>(pin + off);
@@ -1251,33 +1086,25 @@ __device__ __forceinline__ void crypt_block(const BlockKey* __restrict__ bk, con
       uint32_t cw[4];
 #pragma unroll
       for (int i = 0; i < 4; i++) cw[i] = SEAL ? o4[i] : w[i];
-      if (FULL) {
-        pstep32(h32, cw[0], cw[1], cw[2], cw[3], rc);
+      if (L == 16u) {
+        padd_full(h, cw[0], cw[1], cw[2], cw[3]);
       } else {
-        if (L == 16u) {
-          padd_full(h, cw[0], cw[1], cw[2], cw[3]);
-        } else {
-          cw[L >> 2] |= 1u << (8u * (L & 3u));
-          padd_part(h, cw[0], cw[1], cw[2], cw[3]);
-        }
-        h = pmul_u(h, Mr);
+        cw[L >> 2] |= 1u << (8u * (L & 3u));
+        padd_part(h, cw[0], cw[1], cw[2], cw[3]);
       }
+      h = pmul_u(h, Mr);
       c_last = c;
     }
   }
   // bring the lane's partial sum to exponent 0: * r^(nc-1-c_last)
-  if (!FULL) {
-    if (c_last >= 0) {
-      const uint32_t e = (uint32_t)(nc - 1 - c_last);
+  if (c_last >= 0) {
+    const uint32_t e = (uint32_t)(nc - 1 - c_last);
 #pragma unroll
-      for (int i = 0; i < 5; i++) {
-        t1.v[i] = bk->part.T1[e & 31u][i];
-        t2.v[i] = bk->part.T2[e >> 5][i];
-      }
-      h = pmul(h, pmul(t1, t2));
+    for (int i = 0; i < 5; i++) {
+      t1.v[i] = bk->part.T1[e & 31u][i];
+      t2.v[i] = bk->part.T2[e >> 5][i];
     }
-  } else {
-    h = pmul(to26(h32), pmul(t1, t2));
+    h = pmul(h, pmul(t1, t2));
   }
 }
 
@@ -1406,27 +1233,10 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
     for (int mt = 0; mt < 2; mt++)
 #pragma unroll
       for (int i = 0; i < 4; i++) acc[j][mt][i] = lead ? 1 << 24 : 0;  // the bias once per block
-#if XS_DBUF
-  static_assert(NSPLIT == 1, "XS_DBUF is a whole-block-per-wave variant");
-  // double-buffered staging: group u+1 is requested before group u's keystream is computed
-#pragma unroll
-  for (int j = 0; j < 4; j++)
-    if (j > 0 || not_key)
-      __builtin_amdgcn_global_load_lds(pin_m32 + lane_off + 1024 * j, (lds_void*)(wb + 256 * j), 16, 0, 0);
-#endif
 #pragma unroll 1
   for (int u = u_begin; u < u_end; u++) {
     const uint32_t K = 64u * u + l;
     const uint32_t goff = 4096u * (uint32_t)u + lane_off;
-#if XS_DBUF
-    uint32_t* sb = wb + 1024 * (u & 1);
-    if (u < 15) {
-      uint32_t* nb = wb + 1024 * ((u + 1) & 1);
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        __builtin_amdgcn_global_load_lds(pin_m32 + goff + 4096u + 1024 * j, (lds_void*)(nb + 256 * j), 16, 0, 0);
-    }
-#else
     uint32_t* sb = wb;
     // one 64-bit address per group: the four 1 KiB loads differ only in the instruction's
     // immediate offset (no address VALU per load).  The hardware adds that offset to the LDS
@@ -1436,18 +1246,10 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
     __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)sb, 16, 1024, 0);
     __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)sb, 16, 2048, 0);
     __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)sb, 16, 3072, 0);
-#endif
     uint32_t ks[16];
     salsa20_block_pre(pre, K, ks);
-#if XS_DBUF
-    if (u < 15) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // group u landed; u+1 may be in flight
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
     uint4* mine = reinterpret_cast<uint4*>(sb + 256 * (l >> 4) + 4 * (l & 15u));
-#if XS_LDS_XOR
-    static_assert(!XS_ST_PERM && !XS_DBUF, "LDS XOR works on the single staging slot");
     // The data XOR and the MFMA operand's sign bias (C = 0x80 in every byte) run on the LDS's own
     // ALU: 64-bit atomic XORs on this lane's staged words, so the VALU issues no XOR for either
     // (512 fewer VALU instructions per block; paired A/B in DESIGN.md section 3).  Chunk j, half h
@@ -1491,51 +1293,6 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
       bw[2 * q] = (uint32_t)r64[q];
       bw[2 * q + 1] = (uint32_t)(r64[q] >> 32);
     }
-#else
-    uint32_t d[16];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint4 v = mine[16 * j];
-      d[4 * j] = v.x; d[4 * j + 1] = v.y; d[4 * j + 2] = v.z; d[4 * j + 3] = v.w;
-    }
-    uint32_t o[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) o[i] = d[i] ^ ks[i];
-#endif
-#if XS_LDS_XOR
-#elif XS_ST_PERM
-    {  // outputs leave in load order: 4x4 transpose of (16-lane row, chunk) with lane swaps --
-       // afterwards register chunk j of lane λ holds chunk λ>>4 of lane 16j + (λ&15), i.e.
-       // chunk 64j + perm(λ) of the group
-      uint32_t w[16];
-#pragma unroll
-      for (int i = 0; i < 16; i++) w[i] = o[i];
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        auto a = __builtin_amdgcn_permlane32_swap(w[q], w[8 + q], false, false);
-        auto b = __builtin_amdgcn_permlane32_swap(w[4 + q], w[12 + q], false, false);
-        auto c = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
-        auto e = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
-        w[q] = c[0]; w[4 + q] = c[1]; w[8 + q] = e[0]; w[12 + q] = e[1];
-      }
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (j > 0 || u > 0 || not_key)
-          *reinterpret_cast<uint4*>(pout_m32 + goff + 1024 * j) = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
-    }
-#else
-    {  // outputs back through the staging positions, then out in load order
-#pragma unroll
-      for (int j = 0; j < 4; j++) mine[16 * j] = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
-      asm volatile("" ::: "memory");  // LDS ops of one wave execute in order
-      uint4 w[4];
-#pragma unroll
-      for (int j = 0; j < 4; j++) w[j] = *reinterpret_cast<const uint4*>(sb + 256 * j + 4 * l);
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (j > 0 || u > 0 || not_key) *reinterpret_cast<uint4*>(pout_m32 + goff + 1024 * j) = w[j];
-    }
-#endif
     // A operands of row 4u + kg for both output halves
     const lds_u32* zr = zl + 48u * u;
     uint32_t z[9];
@@ -1547,18 +1304,11 @@ __device__ __forceinline__ bool crypt_block_mfma(const BlockKey* __restrict__ bk
       A[1][i] = (int)__builtin_amdgcn_alignbyte(z[i + 1], z[i], zsh);
       A[0][i] = (int)__builtin_amdgcn_alignbyte(z[i + 5], z[i + 4], zsh);
     }
-#if !XS_LDS_XOR
-    const uint32_t* cw = SEAL ? o : d;
-#endif
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       xs_v4i B;
 #pragma unroll
-#if XS_LDS_XOR
       for (int i = 0; i < 4; i++) B[i] = (int)bw[4 * j + i];
-#else
-      for (int i = 0; i < 4; i++) B[i] = (int)(cw[4 * j + i] ^ 0x80808080u);
-#endif
 #pragma unroll
       for (int mt = 0; mt < 2; mt++) {
         acc[j][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[mt], B, acc[j][mt], 0, 0, 0);
@@ -1672,14 +1422,8 @@ __device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, ui
                                            uint8_t* __restrict__ ok, uint32_t* lds) {
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63u;
   // wave-uniform block index
-#if XS_XCD_REMAP
-  // workgroups are dealt round-robin over the 8 XCDs: give each XCD one contiguous range of
-  // blocks (bijective for any grid size) so its L2 / TLB working set moves linearly
-  const uint32_t nwg = gridDim.x, q = nwg >> 3, rem = nwg & 7u, xcd = blockIdx.x & 7u;
-  const uint32_t wg = (xcd < rem ? xcd * (q + 1u) : rem * (q + 1u) + (xcd - rem) * q) + (blockIdx.x >> 3);
-#else
+  // blocks in workgroup order: a contiguous-range-per-XCD remap measured no gain
   const uint32_t wg = blockIdx.x;
-#endif
   const uint64_t blk = FUSED ? (uint64_t)blockIdx.x
                      : NSPLIT == 1 ? (uint64_t)wg * 4u + (uint64_t)__builtin_amdgcn_readfirstlane(wave) : (uint64_t)wg;
   if (blk >= nblocks) return;
@@ -1698,15 +1442,11 @@ __device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, ui
 
   P5 h;
   h.v[0] = h.v[1] = h.v[2] = h.v[3] = h.v[4] = 0;
-#if XS_POLY_MFMA
   if (n == XS_BLOCK_DATA) {
     if (!crypt_block_mfma<SEAL, NSPLIT>(bk, pin, pout, wb, wb + STAGE_WORDS, h, wave, lds)) return;
+  } else {
+    crypt_block<SEAL>(bk, pin, pout, n, wb, h);
   }
-#else
-  static_assert(NSPLIT == 1, "split mode needs the matrix-core Poly1305");
-  if (n == XS_BLOCK_DATA) crypt_block<SEAL, true>(bk, pin, pout, n, wb, h);
-#endif
-  else crypt_block<SEAL, false>(bk, pin, pout, n, wb, h);
 
   // sum the 64 partials with wave shuffles (limbs < 2^26+2^6 -> < 2^32 after 5 levels)
 #pragma unroll
@@ -1744,33 +1484,12 @@ __device__ __forceinline__ void crypt_wave(const BlockKey* __restrict__ keys, ui
   }
 }
 
-#ifdef XS_CLOCK_PROBE
-// Diagnostic build only (tools/ablate.cpp): wave 0 of every workgroup records the shader
-// clock (s_memtime) and the 100 MHz constant clock (s_memrealtime) at entry and exit, giving
-// the sustained shader clock under this kernel's own load.
-__device__ unsigned long long xs_probe[4 * 65536];
-#define XS_PROBE_BEGIN                                                   \
-  const unsigned long long pt0 = __builtin_amdgcn_s_memtime();           \
-  const unsigned long long pr0 = __builtin_amdgcn_s_memrealtime();
-#define XS_PROBE_END                                                     \
-  if (threadIdx.x == 0 && blockIdx.x < 65536) {                          \
-    xs_probe[4 * blockIdx.x + 0] = pt0;                                  \
-    xs_probe[4 * blockIdx.x + 1] = pr0;                                  \
-    xs_probe[4 * blockIdx.x + 2] = __builtin_amdgcn_s_memtime();         \
-    xs_probe[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();     \
-  }
-#else
-#define XS_PROBE_BEGIN
-#define XS_PROBE_END
-#endif
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XS_SEAL_WPE)))
 xs_seal(const BlockKey* __restrict__ keys, uint64_t nblocks, const uint8_t* __restrict__ src,
         uint8_t* __restrict__ dst) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
-  XS_PROBE_BEGIN
   crypt_wave<true, 1>(keys, nblocks, src, dst, nullptr, lds);
-  XS_PROBE_END
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XS_OPEN_WPE)))
@@ -1780,12 +1499,6 @@ xs_open(const BlockKey* __restrict__ keys, uint64_t nblocks, const uint8_t* __re
   crypt_wave<false, 1>(keys, nblocks, src, dst, ok, lds);
 }
 
-#if XS_POLY_MFMA
-// Small batches (latency: a lone ranged read, a few coalesced handles): one block per
-// workgroup, four waves on four super-iterations each.
-// Tiny descriptor batches (ranged reads): keygen and the split crypt kernel in one launch.  Wave 0
-// builds the block's key schedule in LDS (keygen_wave), then the four waves seal / open it as
-// xs_seal_split / xs_open_split do.  Saves the second launch and the key schedule's HBM round trip.
 // Completion word of a fused batch (every wave of every workgroup reaches it): each wave's outputs
 // are fenced at system scope; a one-block batch has no other workgroup to count, otherwise the last
 // workgroup to arrive signals.  The system-scope release of the word orders it after this
@@ -1803,23 +1516,8 @@ __device__ __forceinline__ void xs_fused_complete(uint32_t* ctr, uint32_t* flag,
   }
 }
 
-template <bool SEAL>
-__global__ void __launch_bounds__(256) xs_crypt_fused(KeyArg key, NonceArg bounds, const xs_block_desc* __restrict__ desc,
-                                                      uint64_t nblocks, const uint8_t* __restrict__ src,
-                                                      uint8_t* __restrict__ dst, uint8_t* __restrict__ ok,
-                                                      uint32_t* __restrict__ ctr, uint32_t* __restrict__ flag,
-                                                      uint32_t seq) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
-  __shared__ BlockKey kl;
-  if (blockIdx.x >= nblocks) return;  // uniform per workgroup (grid == nblocks)
-  if (threadIdx.x < 64) keygen_wave<SEAL ? 2 : 3>(key, bounds, 0, 0, desc, blockIdx.x, &kl);
-  __syncthreads();
-  crypt_wave<SEAL, 4, true>(&kl, nblocks, src, dst, ok, lds);
-  if (ctr) xs_fused_complete(ctr, flag, seq, nblocks);
-}
-
-// Tiny descriptor batches, latency-first (XS_FUSED_V 3, default; 2 = the four-crypt-wave form):
-// one workgroup per block.  Descriptors of batches of <= 16 blocks arrive in the kernel arguments.
+// Tiny descriptor batches (ranged reads, a few coalesced handles), latency-first: one workgroup
+// per block, keygen and crypt in one launch.  Descriptors of batches of <= 16 blocks arrive in the kernel arguments.
 // For a full block the crypt waves start at once on the data: each stages its 4 KiB groups with
 // LDS-DMA (one PCIe round trip for all of them), derives the HSalsa20 subkey (or takes it from the
 // wave on its SIMD that did) and runs its keystream blocks, writing the output and keeping the
@@ -1831,31 +1529,27 @@ __global__ void __launch_bounds__(256) xs_crypt_fused(KeyArg key, NonceArg bound
 // LDS and wave 0 finalises as crypt_block_mfma does (the two tail chunks' terms were computed
 // while it waited).  The key schedule thus leaves the critical path.  Cross-wave hand-offs are
 // LDS flags raised after lgkmcnt(0) and polled with inline ds_reads, never release / acquire
-// (those would wait for the waves' outstanding PCIe loads).  Partial blocks take the fused-v1
-// order (key schedule, then wave 0's VALU path).  Phase timings: tools/fused_probe.cpp.
-// NCW crypt waves (4: v2, one per SIMD; 8: v3, two per SIMD so that each SIMD interleaves two
-// dependency chains) plus the key-schedule wave NCW.  Crypt wave w runs on SIMD w % 4; SIMD 0 also
-// runs the key-schedule wave (the longer chain, tools/fused_probe.cpp), so its crypt waves take
-// fewer 4 KiB groups.  Group counts per wave, 4 bits each (wave 0 first), and first groups, 8 bits:
-//   NCW 4: {1, 5, 5, 5}                 -> SIMD loads 1, 5, 5, 5
-//   NCW 8: {1, 3, 3, 3, 0, 2, 2, 2}     -> SIMD loads 1, 5, 5, 5 (wave 4 idles until phase 2)
-// With NCW 8, waves 4..7 take the HSalsa20 subkey from wave w - 4 (same SIMD) through LDS instead
-// of computing it again: a SIMD's second wave only gets the issue slots its first leaves.
-#ifndef XS_F3_DIST  // NCW 8 group split: 0 = {1, 3, 3, 3, 0, 2, 2, 2}; 1 = two groups per crypt wave
-#define XS_F3_DIST 0
-#endif
+// (those would wait for the waves' outstanding PCIe loads).  Partial blocks (and rejected
+// descriptors) take the plain order: key schedule, then wave 0's VALU path.
+// NCW = 8 crypt waves, two per SIMD so that each SIMD interleaves two dependency chains, plus the
+// key-schedule wave NCW.  Crypt wave w runs on SIMD w % 4; SIMD 0 also runs the key-schedule wave
+// (the longer chain), so its crypt waves take fewer 4 KiB groups.  Group counts per wave, 4 bits
+// each (wave 0 first), and first groups, 8 bits:
+//   {1, 3, 3, 3, 0, 2, 2, 2}  -> SIMD loads 1, 5, 5, 5 (wave 4 idles until phase 2)
+// Waves 4..7 take the HSalsa20 subkey from wave w - 4 (same SIMD) through LDS instead of computing
+// it again: a SIMD's second wave only gets the issue slots its first leaves.  (One crypt wave per
+// SIMD, and an even two groups per wave, measured slower: DESIGN.md section 3e.)
 template <int NCW>
 __device__ __forceinline__ uint32_t f2_count(uint32_t w) {
-  constexpr uint32_t c = NCW == 4 ? 0x5551u : XS_F3_DIST ? 0x22222222u : 0x22203331u;
-  return (c >> (4u * w)) & 15u;
+  static_assert(NCW == 8, "the group split below is for eight crypt waves");
+  return (0x22203331u >> (4u * w)) & 15u;
 }
 template <int NCW>
 __device__ __forceinline__ uint32_t f2_first(uint32_t w) {
-  constexpr uint64_t f = NCW == 4 ? 0x0B060100ull : XS_F3_DIST ? 0x0E0C0A0806040200ull : 0x0E0C0A0A07040100ull;
-  return (uint32_t)(f >> (8u * w)) & 255u;
+  return (uint32_t)(0x0E0C0A0A07040100ull >> (8u * w)) & 255u;
 }
 template <int NCW>
-constexpr int f2_max_groups() { return NCW == 4 ? 5 : XS_F3_DIST ? 2 : 3; }
+constexpr int f2_max_groups() { return 3; }
 // LDS words: stage (16 groups of 4 KiB, indexed by group), relay (4 KiB per crypt wave), the
 // accumulators of crypt waves 1..NCW-1 (8 KiB each), the Toeplitz digit rows (3 KiB)
 template <int NCW>
@@ -1889,22 +1583,6 @@ __device__ __forceinline__ void wave_sum5(P5& h) {
   }
 }
 
-#ifdef XS_F2_PROBE
-// Diagnostic build only (tools/fused_probe.cpp): s_memrealtime (100 MHz) at phase boundaries, per
-// wave of workgroup 0, lane-indexed vector stores.
-__device__ unsigned long long xs_f2_probe[2 * 10 * 16];  // [clock][wave 0..9][slot]; row 9: keygen_wave
-#define F2_MARK(slot)                                                                        \
-  do {                                                                                       \
-    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                          \
-    const unsigned long long c_ = __builtin_amdgcn_s_memtime();                              \
-    if (blockIdx.x == 0 && l < 2u) xs_f2_probe[160 * l + 16 * wave + (slot)] = l ? c_ : t_;   \
-  } while (0)
-#else
-#define F2_MARK(slot) \
-  do {                \
-  } while (0)
-#endif
-
 template <bool SEAL, int NCW>
 __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, NonceArg bounds, const xs_block_desc* __restrict__ desc,
                                                                     const XsInlineDescs inl,
@@ -1923,7 +1601,6 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63u;
   const uint64_t blk = blockIdx.x;
   if (threadIdx.x < 6u) hs_flag[threadIdx.x] = 0u;
-  F2_MARK(0);
   uint32_t nn[6];
   uint64_t soff, doff;
   uint32_t len;
@@ -1950,7 +1627,6 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
   }
   gwin = __builtin_amdgcn_readfirstlane(gwin);
   __syncthreads();  // hs_flag cleared before any wave can poll or raise it
-  F2_MARK(1);
   if (!valid || len != XS_BLOCK_DATA) {
     // rejected descriptor or partial block: the fused-v1 order (the other waves idle)
     if (wave == 0) {
@@ -2001,7 +1677,6 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
         tail[0] = *reinterpret_cast<const uint4*>(tp);
         tail[1] = *reinterpret_cast<const uint4*>(tp + 16);
       }
-      F2_MARK(14);
       uint32_t sk[8];
       if (NCW == 8 && wave >= 4u) {  // the subkey of wave - 4, which shares this SIMD
         if (gn != 0u) lds_wait_subkey(&hs_flag[wave - 4u], hs_key[wave - 4u], sk);
@@ -2019,9 +1694,7 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
         }
         lds_raise_flag(&hs_flag[wave]);
       }
-      F2_MARK(15);
       const SalsaPre pre = salsa_pre(sk, nn[4], nn[5]);
-      F2_MARK(2);
       uint32_t* const rl = relay + 1024 * wave;
 #pragma unroll 1
       for (uint32_t g = 0; g < gn; g++) {
@@ -2029,9 +1702,7 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
         if (!((gwin >> u) & 1u)) continue;  // outside the window: staged for the tag only
         uint32_t ks[16];
         salsa20_block_pre(pre, 64u * u + l, ks);
-        F2_MARK(3 + 2 * g);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        F2_MARK(4 + 2 * g);
         uint32_t* sb = stage + 1024 * u;
         uint4* mine = reinterpret_cast<uint4*>(sb + 256 * (l >> 4) + 4 * (l & 15u));
         uint32_t o[16];
@@ -2059,7 +1730,6 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
             *reinterpret_cast<uint4*>(pout_m32 + 4096u * u + lane_off + 1024 * j) = w[j];
       }
       if (!SEAL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // plaintext out before any zero-fill
-      F2_MARK(11);
     } else {
       // ---- the key wave: key schedule into LDS; as soon as the A and B power tables exist, the
       // shared Toeplitz digit table and the Z-ready flag (the crypt waves' MFMA phase needs no
@@ -2067,7 +1737,6 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
       // It shares a SIMD with wave 0 and is the longer chain: it issues first.
       __builtin_amdgcn_s_setprio(3);
       auto z_table = [&]() {
-        F2_MARK(2);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2095,7 +1764,6 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
         row[1] = make_uint4(__builtin_bswap32(w3), __builtin_bswap32(w2), __builtin_bswap32(w1), __builtin_bswap32(w0));
         row[2] = make_uint4(0u, 0u, 0u, 0u);
         lds_raise_flag(&hs_flag[4]);
-        F2_MARK(3);
       };
       // the descriptor fields this kernel already holds (no second read over PCIe); wave 0's subkey
       keygen_wave_body<MODE>(key, nn, soff, doff, len, &kl, hs_key[0], &hs_flag[0], z_table, &hs_flag[5]);
@@ -2106,7 +1774,6 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
     for (int i = 0; i < 5; i++) tl.v[i] = 0;
     if (wave < NCW) {
       lds_wait_flag(&hs_flag[4]);  // the Z table (each wave reads only its own staged groups)
-      F2_MARK(12);
       if (wave == 0 && l == 63u) {
         // chunks 4094, 4095 (keystream block 1024 words 0..7): exponents 2 and 1.  r and ks1024
         // are in kl before the Z flag rises, so this leaves the finalisation's critical path.
@@ -2188,7 +1855,6 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
       rexp = pmul(t2, t1);
     }
     __syncthreads();  // B2: the other waves' accumulators are in LDS
-    F2_MARK(13);
     if (wave == 0) {
 #pragma unroll
       for (int w = 0; w < NCW - 1; w++)
@@ -2254,7 +1920,6 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
             *reinterpret_cast<uint4*>(pout + off) = make_uint4(0, 0, 0, 0);
         }
       }
-      F2_MARK(14);
     }
   }
   if (ctr) xs_fused_complete(ctr, flag, seq, nblocks);
@@ -2272,7 +1937,6 @@ __global__ void __launch_bounds__(256) xs_open_split(const BlockKey* __restrict_
   __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_WORDS];
   crypt_wave<false, 4>(keys, nblocks, src, dst, ok, lds);
 }
-#endif
 
 // SplitMix64 fill (synthetic benchmark objects generated in HBM).  Global word g of the stream
 // is mix(seed + (g+1)*golden); local 64 KiB block b of the buffer holds global block
@@ -2319,16 +1983,9 @@ hipError_t launch_keygen(int mode, const KeyArg& key, const NonceArg& nonce0, ui
   return hipGetLastError();
 }
 
-#ifdef XS_CLOCK_PROBE
-void probe_read(unsigned long long* host, size_t n) {
-  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(xs_probe), n * sizeof(unsigned long long));
-}
-#endif
-
 hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const uint8_t* src, uint8_t* dst,
                         uint8_t* ok, hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
-#if XS_POLY_MFMA
   static const uint64_t split_max = [] {  // env XS_SPLIT_MAX overrides (A/B, 0 = never)
     const char* v = getenv("XS_SPLIT_MAX");
     return v ? strtoull(v, nullptr, 10) : (uint64_t)XS_SPLIT_MAX;
@@ -2338,7 +1995,6 @@ hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const
     else hipLaunchKernelGGL(xs_open_split, dim3((unsigned)nblocks), dim3(256), 0, stream, keys, nblocks, src, dst, ok);
     return hipGetLastError();
   }
-#endif
   const unsigned grid = (unsigned)((nblocks + 3) / 4);  // four blocks (waves) per workgroup
   if (seal) hipLaunchKernelGGL(xs_seal, dim3(grid), dim3(256), 0, stream, keys, nblocks, src, dst);
   else hipLaunchKernelGGL(xs_open, dim3(grid), dim3(256), 0, stream, keys, nblocks, src, dst, ok);
@@ -2354,35 +2010,18 @@ hipError_t launch_crypt_fused(bool seal, const KeyArg& key, const NonceArg& boun
     for (uint64_t i = 0; i < nblocks; i++) inl.d[i] = host_desc[i];
     inl.n = (uint32_t)nblocks;
   }
-  static const int version = [] {  // env XS_FUSED_V: 1 = keygen then split crypt, 2 / 3 = overlapped (A/B)
-    const char* v = getenv("XS_FUSED_V");
-    return v ? atoi(v) : XS_FUSED_V;
-  }();
-  if (version >= 3) {  // eight crypt waves (two per SIMD) + the key-schedule wave
-    if (seal) hipLaunchKernelGGL((xs_crypt_fused2<true, 8>), dim3((unsigned)nblocks), dim3(576), 0, stream, key, bounds, desc, inl, nblocks, src, dst, ok, ctr, flag, seq);
-    else hipLaunchKernelGGL((xs_crypt_fused2<false, 8>), dim3((unsigned)nblocks), dim3(576), 0, stream, key, bounds, desc, inl, nblocks, src, dst, ok, ctr, flag, seq);
-    return hipGetLastError();
-  }
-  if (version == 2) {  // four crypt waves (one per SIMD) + the key-schedule wave
-    if (seal) hipLaunchKernelGGL((xs_crypt_fused2<true, 4>), dim3((unsigned)nblocks), dim3(320), 0, stream, key, bounds, desc, inl, nblocks, src, dst, ok, ctr, flag, seq);
-    else hipLaunchKernelGGL((xs_crypt_fused2<false, 4>), dim3((unsigned)nblocks), dim3(320), 0, stream, key, bounds, desc, inl, nblocks, src, dst, ok, ctr, flag, seq);
-    return hipGetLastError();
-  }
-  if (seal) hipLaunchKernelGGL(xs_crypt_fused<true>, dim3((unsigned)nblocks), dim3(256), 0, stream, key, bounds, desc, nblocks, src, dst, ok, ctr, flag, seq);
-  else hipLaunchKernelGGL(xs_crypt_fused<false>, dim3((unsigned)nblocks), dim3(256), 0, stream, key, bounds, desc, nblocks, src, dst, ok, ctr, flag, seq);
+  // eight crypt waves (two per SIMD) + the key-schedule wave
+  if (seal) hipLaunchKernelGGL((xs_crypt_fused2<true, 8>), dim3((unsigned)nblocks), dim3(576), 0, stream, key, bounds, desc, inl, nblocks, src, dst, ok, ctr, flag, seq);
+  else hipLaunchKernelGGL((xs_crypt_fused2<false, 8>), dim3((unsigned)nblocks), dim3(576), 0, stream, key, bounds, desc, inl, nblocks, src, dst, ok, ctr, flag, seq);
   return hipGetLastError();
 }
 
 uint64_t fused_max_blocks() {
-#if XS_POLY_MFMA
   static const uint64_t m = [] {  // env XS_FUSED_MAX overrides (A/B, 0 = never)
     const char* v = getenv("XS_FUSED_MAX");
     return v ? strtoull(v, nullptr, 10) : (uint64_t)XS_FUSED_MAX;
   }();
   return m;
-#else
-  return 0;  // the split kernels need the matrix-core Poly1305
-#endif
 }
 
 hipError_t launch_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t first_block, uint64_t stride,

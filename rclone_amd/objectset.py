@@ -32,6 +32,10 @@ CONFIG3_KEY = bytes(range(100, 132))
 CONFIG3_NONCE0 = b"\xf0" + b"\xff" * 7 + bytes(range(16))  # the set's nonces carry across byte 8
 CONFIG3_SEED = 0x1417
 CONFIG3_ROUND_BLOCKS = 100_000
+# the order-independent tag digest of one pass over that set (hi || lo, hex), measured on the GPU by
+# tests/test_objectset_gpu.py at world 1, 2 and 8 (equal for all three; each rank's last block is
+# checked against the CPU oracle there): a regression anchor for the test and the bench leg
+CONFIG3_TAG_DIGEST = "26763293cb7e88a920e9c78b28f3f58d"
 
 
 def _descriptors(nonce0: bytes, gidx: np.ndarray, round_blocks: int, open_mode: bool) -> np.ndarray:
@@ -119,6 +123,10 @@ class RankRunner:
         self.kernel_events.append((seal, a, b))
 
     def run_all(self, record: bool = False):
+        """One pass over the rank's share.  Blocks, bytes, failures and mismatches accumulate over
+        passes; the tag digest (counters 4:6) is the latest pass's, so it is comparable across runs
+        of any length (one 16-byte clear per pass)."""
+        self.counters[4:6].zero_()
         for k in range(self.rounds):
             self.run_round(k, record)
         return self.counters

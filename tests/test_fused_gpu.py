@@ -1,12 +1,12 @@
 """The fused small-batch kernels (ranged reads: keygen + crypt in one launch).
 
-Tiny zero-copy engine batches (one key, one direction, <= XS_FUSED_MAX blocks) run one launch:
-XS_FUSED_V=1 builds the key schedule first and then runs the four-wave split crypt; XS_FUSED_V=2
-(default) overlaps the key schedule (wave 4) with the keystream work of waves 0..3 and runs the
-matrix-core Poly1305 over the LDS-resident ciphertext afterwards.  Both must give the oracle's
-bytes, tags and verdicts for every tail length, carry nonces, first_block offsets, multi-block
-batches and tampered tags / ciphertext / nonces.  Each version runs in its own process (the
-version is read once per process).
+Tiny zero-copy engine batches (one key, one direction, <= XS_FUSED_MAX blocks) run one launch
+(xs_crypt_fused2: eight crypt waves overlap the keystream with the key-schedule wave and run the
+matrix-core Poly1305 over the LDS-resident ciphertext afterwards).  With XS_FUSED_MAX=0 the same
+batches take two launches instead (keygen, then the four-wave split crypt).  Both must give the
+oracle's bytes, tags and verdicts for every tail length, carry nonces, first_block offsets,
+multi-block batches and tampered tags / ciphertext / nonces, and the same digest.  Each setting
+runs in its own process (the threshold is read once per process).
 """
 import json
 import os
@@ -146,10 +146,10 @@ print(json.dumps({"bad": bad[:10], "nbad": len(bad), "cases": cases, "digest": h
 """
 
 
-def _run(version):
+def _run(fused_max):
     # the leader holds new requests while a batch is in flight and express lanes are off, so the
     # concurrent phase forms multi-request fused batches (the path this test is about)
-    env = dict(os.environ, XS_FUSED_V=str(version), XS_ENGINE_ZERO_COPY="1", XS_ENGINE_COALESCE="1",
+    env = dict(os.environ, XS_FUSED_MAX=str(fused_max), XS_ENGINE_ZERO_COPY="1", XS_ENGINE_COALESCE="1",
                XS_ENGINE_OVERLAP="0", XS_EXPRESS_MAX="0")
     r = subprocess.run([sys.executable, "-c", SCRIPT % {"root": ROOT}], capture_output=True, text=True, timeout=240,
                        env=env, cwd=ROOT)
@@ -158,15 +158,15 @@ def _run(version):
 
 
 @pytest.mark.timeout(600)
-def test_fused_versions_agree_with_oracle():
+def test_fused_and_two_launch_paths_agree_with_oracle():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    v1, v2, v3 = _run(1), _run(2), _run(3)
-    for v in (v1, v2, v3):
+    fused, split = _run(16), _run(0)
+    for v in (fused, split):
         assert v["bad"] == [], (v["nbad"], v["bad"])
-    assert v2["concurrent"]["batches"] < v2["concurrent"]["requests"]  # the concurrent opens did coalesce
-    assert v1["cases"] == v2["cases"] == v3["cases"] > 150
-    assert v1["digest"] == v2["digest"] == v3["digest"]
+    assert fused["concurrent"]["batches"] < fused["concurrent"]["requests"]  # the concurrent opens did coalesce
+    assert fused["cases"] == split["cases"] > 150
+    assert fused["digest"] == split["digest"]
 
 
 def test_first_fused_open_on_fresh_engines_reports_tampering():

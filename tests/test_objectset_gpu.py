@@ -20,7 +20,8 @@ from rclone_amd.testdata import splitmix64_block
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-from rclone_amd.objectset import CONFIG3_BLOCKS, CONFIG3_KEY, CONFIG3_NONCE0, CONFIG3_SEED  # noqa: E402
+from rclone_amd.objectset import (CONFIG3_BLOCKS, CONFIG3_KEY, CONFIG3_NONCE0, CONFIG3_SEED,  # noqa: E402
+                                  CONFIG3_TAG_DIGEST)
 
 TOTAL = int(os.environ.get("RCLONE_AMD_OBJECTSET_BLOCKS", CONFIG3_BLOCKS))
 SEED = CONFIG3_SEED
@@ -51,6 +52,9 @@ def test_objectset_digest_independent_of_world():
         # the same string bench.py's objectset leg reports (counters.tag_digest)
         print(f"configs[3] world {world}: {TOTAL} blocks, tag_digest {d1:016x}{d0:016x}")
     assert res[1] == res[2] == res[8]
+    if TOTAL == CONFIG3_BLOCKS:  # the anchor bench.py's objectset leg is held to
+        d0, d1 = res[1]
+        assert f"{d1:016x}{d0:016x}" == CONFIG3_TAG_DIGEST
 
 
 def test_verify_blocks_counts_mismatched_words():

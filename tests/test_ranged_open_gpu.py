@@ -2,12 +2,12 @@
 
 The decrypter opens the block a RangeSeek lands in (cipher.go:972-1034) knowing that Reads will
 serve plaintext bytes [discard, discard + limit) of it at most.  Through xs_engine_open_range the
-fused kernels (XS_FUSED_V 2 and 3) then run the keystream over the 4 KiB groups covering that
-range only, while the Poly1305 tag is still computed over the whole block.  Checked against the
-oracle for every version, with XS_FUSED_MAX=0 (no fused kernel: every byte written) as the
-control: bytes inside the range and every verdict equal the oracle's, a tampered block is
-zero-filled whole, and -- for the fused versions on full blocks -- groups outside the window keep
-the caller's sentinel bytes (the window was honoured, not just tolerated).
+fused kernel (xs_crypt_fused2) then runs the keystream over the 4 KiB groups covering that range
+only, while the Poly1305 tag is still computed over the whole block.  Checked against the oracle,
+with XS_FUSED_MAX=0 (no fused kernel: every byte written) as the control: bytes inside the range
+and every verdict equal the oracle's, a tampered block is zero-filled whole, and -- for the fused
+kernel on full blocks -- groups outside the window keep the caller's sentinel bytes (the window
+was honoured, not just tolerated).
 """
 import json
 import os
@@ -95,20 +95,20 @@ print(json.dumps({"bad": bad[:10], "nbad": len(bad), "cases": cases, "skipped_gr
 """
 
 
-def _run(version, fused_max):
-    env = dict(os.environ, XS_FUSED_V=str(version), XS_FUSED_MAX=str(fused_max), XS_ENGINE_ZERO_COPY="1")
-    r = subprocess.run([sys.executable, "-c", SCRIPT % {"root": ROOT, "fused": 1 if fused_max and version >= 2 else 0}],
+def _run(fused_max):
+    env = dict(os.environ, XS_FUSED_MAX=str(fused_max), XS_ENGINE_ZERO_COPY="1")
+    r = subprocess.run([sys.executable, "-c", SCRIPT % {"root": ROOT, "fused": 1 if fused_max else 0}],
                        capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("version,fused_max", [(3, 16), (2, 16), (3, 0)])
-def test_ranged_open_matches_oracle(version, fused_max):
+@pytest.mark.parametrize("fused_max", [16, 0])
+def test_ranged_open_matches_oracle(fused_max):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    v = _run(version, fused_max)
+    v = _run(fused_max)
     assert v["bad"] == [], (v["nbad"], v["bad"])
     assert v["cases"] > 400
     if fused_max:

@@ -39,20 +39,5 @@ int main(int argc, char** argv) {
            dir ? "open" : "seal", t[0], t[12], nb * 65536.0 / 1073741824.0 / (t[12] * 1e-3),
            hipGetErrorString(hipGetLastError()));
   }
-#ifdef XS_CLOCK_PROBE
-  // last launch was open; re-run one seal and read the per-workgroup clocks
-  (void)xs::launch_crypt(true, ws, nb, plain, body, nullptr, 0);
-  (void)hipDeviceSynchronize();
-  const size_t nwg = (nb + 3) / 4;
-  std::vector<unsigned long long> pr(4 * nwg);
-  xs::probe_read(pr.data(), pr.size());
-  double sum = 0, mn = 1e30, mx = 0;
-  for (size_t i = 0; i < nwg; i++) {
-    const double f = (double)(pr[4 * i + 2] - pr[4 * i]) / (double)(pr[4 * i + 3] - pr[4 * i + 1]) * 100e6;
-    sum += f; mn = f < mn ? f : mn; mx = f > mx ? f : mx;
-  }
-  printf("shader clock under seal load: mean %.3f GHz  min %.3f  max %.3f  (%zu workgroups)\n", sum / nwg / 1e9,
-         mn / 1e9, mx / 1e9, nwg);
-#endif
   return 0;
 }

@@ -19,11 +19,22 @@ def main():
     for line in open(log):
         if line.startswith("{"):
             bench = json.loads(line)
-    res = {"steps": steps}
+    # the configs[3] leg (bench.py objectset_leg) runs after the headline timing: its launches
+    # (warm-up + timed passes x rounds per pass) come last in the trace and are skipped
+    tail = 0
+    os_ = bench.get("objectset")
+    if os_:
+        per_rank = -(-os_["counters"]["blocks"] // os_["steps"] // bench["n_gpus"])
+        rounds = -(-per_rank // 100_000)
+        tail = (os_["steps"] + os_["warmup"]) * rounds
+    res = {"steps": steps, "objectset_launches_skipped": tail}
     ev = {"xs_seal": bench["roofline"]["kernel_ms_avg"], "xs_open": bench["roofline"]["open"]["kernel_ms_avg"]}
     for name in ("xs_seal", "xs_open"):
-        dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows if name in r["Kernel_Name"]]
+        dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows if name in r["Kernel_Name"]
+               and "split" not in r["Kernel_Name"]]
         dur_sorted = dur  # trace rows are in dispatch order per file
+        if tail:
+            dur_sorted = dur_sorted[:-tail]
         timed = dur_sorted[-steps:]
         avg = sum(timed) / len(timed)
         res[name] = {"rocprof_timed_avg_ms": round(avg, 4), "rocprof_all_avg_ms": round(sum(dur) / len(dur), 4),
