@@ -109,10 +109,12 @@ int parse_device_list(const char* s, std::vector<int>* out) {
   return (int)out->size();
 }
 
-// The process's CPU affinity as it was when the library was loaded (the loading thread's mask:
-// what the operator gave the process with taskset / numactl / the container).  Library threads
-// are pinned inside it, and effective_cpus() counts it, whichever thread asks later -- a thread
-// the library has already pinned to one node must not shrink either.
+// The process's CPU affinity: the main thread's mask (what the operator gave the process with
+// taskset / numactl / the container, and what `taskset -p` or a cpuset change moves later), read
+// again whenever the library sizes a pool or pins one of its threads -- so a mask narrowed or
+// widened after load is honoured.  Read by pid, not by the calling thread, so a thread the
+// library has already pinned to one node does not shrink it.  The mask at load is the fallback
+// when the main thread cannot be queried.
 static cpu_set_t g_process_cpus;
 static bool g_process_cpus_ok = false;
 
@@ -122,6 +124,14 @@ void capture_process_affinity() {
 }
 
 [[maybe_unused]] static const bool g_captured_at_load = (capture_process_affinity(), true);
+
+static bool process_cpus(cpu_set_t* set) {
+  CPU_ZERO(set);
+  if (sched_getaffinity(getpid(), sizeof *set, set) == 0 && CPU_COUNT(set) > 0) return true;
+  if (!g_process_cpus_ok) return false;
+  *set = g_process_cpus;
+  return true;
+}
 
 // cgroup v2: the quota that binds this process is the smallest cpu.max on the path from its own
 // group (/proc/self/cgroup "0::/a/b") up to the mount root, so a nested group (a systemd slice
@@ -165,7 +175,7 @@ static double cgroup_v2_quota(const std::string& root) {
   return quota;
 }
 
-// CPUs this process can use: its affinity mask at load, capped by the cgroup CPU quota (v2
+// CPUs this process can use: its affinity mask (as it is now), capped by the cgroup CPU quota (v2
 // cpu.max along the process's own group path, or v1 cpu.cfs_quota_us / cpu.cfs_period_us under
 // the sysfs root); RCLONE_AMD_CPUS overrides.  A GPU box share of 16 cores on a 256-CPU machine
 // is 16, not 256.
@@ -174,7 +184,8 @@ int effective_cpus() {
     const int v = atoi(e);
     if (v > 0) return v;
   }
-  int n = g_process_cpus_ok ? CPU_COUNT(&g_process_cpus) : (int)std::thread::hardware_concurrency();
+  cpu_set_t mask;
+  int n = process_cpus(&mask) ? CPU_COUNT(&mask) : (int)std::thread::hardware_concurrency();
   const std::string root = sysfs_root();
   double quota = cgroup_v2_quota(root);
   if (quota == -2) {
@@ -190,17 +201,18 @@ int effective_cpus() {
 }
 
 // Pin the calling thread to the CPUs of `node` that the process may use (the node's CPU list
-// intersected with the process affinity captured at load).  No-op when the node or its CPU list
+// intersected with the process affinity as it is now).  No-op when the node or its CPU list
 // is unknown, the intersection is empty, or RCLONE_AMD_NUMA=0.  Only threads this library starts
 // are pinned -- never a caller's thread.
 void pin_thread_to_node(int node) {
   if (!numa_enabled()) return;
   std::vector<int> cpus;
   if (!node_cpus(node, &cpus)) return;
-  cpu_set_t set;
+  cpu_set_t mask, set;
+  const bool have_mask = process_cpus(&mask);
   CPU_ZERO(&set);
   for (int c : cpus)
-    if (c < CPU_SETSIZE && (!g_process_cpus_ok || CPU_ISSET(c, &g_process_cpus))) CPU_SET(c, &set);
+    if (c < CPU_SETSIZE && (!have_mask || CPU_ISSET(c, &mask))) CPU_SET(c, &set);
   if (CPU_COUNT(&set) == 0) return;
   (void)sched_setaffinity(0, sizeof set, &set);
 }

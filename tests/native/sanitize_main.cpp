@@ -747,8 +747,27 @@ static void test_topology() {
     });
     t3.join();
     const int counted = xs::effective_cpus();
+    // the mask changes after load (taskset -p / a cpuset update), with no capture call: the next
+    // pool sizing and pinning follow it
+    cpu_set_t one;
+    CPU_ZERO(&one);
+    CPU_SET(2, &one);
+    sched_setaffinity(0, sizeof one, &one);
+    const int counted_one = xs::effective_cpus();
+    int moved_ok = 0;
+    std::thread t4([&] {
+      xs::pin_thread_to_node(3);  // node {0,1} & mask {2} = {}: left on the process mask
+      cpu_set_t s;
+      CPU_ZERO(&s);
+      if (sched_getaffinity(0, sizeof s, &s) == 0) moved_ok = CPU_COUNT(&s) == 1 && CPU_ISSET(2, &s);
+    });
+    t4.join();
     sched_setaffinity(0, sizeof full, &full);
+    const int counted_full = xs::effective_cpus();
     xs::capture_process_affinity();
+    CHECK(counted_one == 1 || getenv("RCLONE_AMD_CPUS"), "effective_cpus follows a mask narrowed after load (%d)", counted_one);
+    CHECK(counted_full >= counted || getenv("RCLONE_AMD_CPUS"), "effective_cpus follows a mask widened again (%d)", counted_full);
+    CHECK(moved_ok, "library threads stay inside the mask as it is now");
     CHECK(inter_ok, "pinning intersects the node with the process mask");
     CHECK(disjoint_ok, "no pinning outside the process mask when the node is disjoint from it");
     CHECK(counted == 2 || getenv("RCLONE_AMD_CPUS"), "effective_cpus counts the process mask (%d)", counted);
