@@ -9,7 +9,8 @@ csrc/, the public header and the compile command -- as the library's build id
 (`xs_build_id()`, and a tagged string the loader reads from the file without loading it).
 `needs_build()` compares that id with the tree's, not file times, so a library built from other
 sources is never taken for this tree's (rclone_amd/_lib.py rebuilds or refuses it).  The compiler
-is stamped beside it (`compiler_id()`: a digest of `hipcc --version`, tag "xs-build-compiler:"): where
+is stamped beside it (`compiler_id()`: a digest of the installed hipcc / clang / ROCm release,
+tag "xs-build-compiler:"): where
 hipcc is installed, a library built by another hipcc / ROCm counts as stale too.  It is kept out of
 the build id so a box without a compiler can still load the library it was given.
 """
@@ -93,16 +94,28 @@ def library_build_id(path=LIB):
 
 
 def compiler_id():
-    """First 16 hex digits of sha256(`$HIPCC --version`), or None without a usable hipcc."""
+    """First 16 hex digits of a sha256 over what identifies the installed compiler -- the resolved
+    hipcc and clang paths, the clang binary's size and the ROCm release files -- or None without a
+    usable hipcc.  Read from the file system, never by running hipcc: the loader runs in processes
+    that have initialised the GPU, where no child program should be started."""
     global _compiler_id
     if _compiler_id is None:
-        try:
-            out = subprocess.run([HIPCC, "--version"], capture_output=True, timeout=60).stdout
-        except (OSError, subprocess.SubprocessError):
+        import shutil
+        hipcc = shutil.which(HIPCC) or HIPCC
+        if not os.path.exists(hipcc):
             return None
-        if not out:
-            return None
-        _compiler_id = hashlib.sha256(out).hexdigest()[:16]
+        real = os.path.realpath(hipcc)
+        rocm = os.path.dirname(os.path.dirname(real))
+        h = hashlib.sha256(real.encode() + b"\0")
+        clang = os.path.realpath(os.path.join(rocm, "lib", "llvm", "bin", "clang"))
+        if os.path.exists(clang):
+            h.update(clang.encode() + b"\0" + str(os.path.getsize(clang)).encode() + b"\0")
+        info = os.path.join(rocm, ".info")
+        if os.path.isdir(info):
+            for f in sorted(os.listdir(info)):
+                with open(os.path.join(info, f), "rb") as fh:
+                    h.update(f.encode() + b"\0" + fh.read() + b"\0")
+        _compiler_id = h.hexdigest()[:16]
     return _compiler_id
 
 

@@ -103,13 +103,11 @@ def test_library_from_another_compiler_is_refused(tmp_path):
 
 
 _FAKE_HIPCC = r"""#!{py}
-# TEST INFRASTRUCTURE: stands in for hipcc -- --version from the real one, '-c' writes an empty
-# object slowly (widens the race), the link copies the real library and is logged
-import os, shutil, subprocess, sys, time
+# TEST INFRASTRUCTURE: stands in for hipcc -- '-c' writes an empty object slowly (widens the race),
+# the link copies a current library (the real one, stamped with this stand-in's compiler id) and
+# is logged
+import os, shutil, sys, time
 args = sys.argv[1:]
-if args == ["--version"]:
-    sys.stdout.write(subprocess.run([{real!r}, "--version"], capture_output=True, text=True).stdout)
-    sys.exit(0)
 out = args[args.index("-o") + 1]
 if "-c" in args:
     time.sleep(0.5)
@@ -145,10 +143,20 @@ def test_concurrent_loaders_rebuild_once(tmp_path):
     (pkg / "librclone_crypt.so").write_bytes(bytes(data))  # stale: another build id
     log = tmp_path / "hipcc.log"
     fake = tmp_path / "hipcc"
-    fake.write_text(_FAKE_HIPCC.format(py=sys.executable, real=build.HIPCC, log=str(log), lib=build.LIB))
+    good = tmp_path / "good.so"
+    fake.write_text(_FAKE_HIPCC.format(py=sys.executable, log=str(log), lib=str(good)))
     fake.chmod(0o755)
-    code = ("import sys; sys.path.insert(0, %r)\nfrom rclone_amd import _lib\nprint('ID', _lib.build_id())" % str(tree))
     env = dict(os.environ, HIPCC=str(fake), RCLONE_AMD_REBUILD="1")
+    # the library the stand-in's link hands back: this tree's build, stamped with the compiler id
+    # the scratch tree computes for the stand-in
+    cc = subprocess.check_output([sys.executable, "-c", "import sys; sys.path.insert(0, %r)\n"
+                                  "from rclone_amd import build; print(build.compiler_id())" % str(tree)],
+                                 env=env, text=True).strip()
+    real = bytearray(open(build.LIB, "rb").read())
+    k = real.index(build.COMPILER_TAG) + len(build.COMPILER_TAG)
+    real[k:k + 16] = cc.encode()
+    good.write_bytes(bytes(real))
+    code = ("import sys; sys.path.insert(0, %r)\nfrom rclone_amd import _lib\nprint('ID', _lib.build_id())" % str(tree))
     procs = [subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                               env=env, cwd=str(tmp_path)) for _ in range(4)]
     outs = [p.communicate(timeout=180) for p in procs]
