@@ -402,7 +402,7 @@ def _pool_check_body(devices):
         return {"devices": n_dev, "ran": True, "ok": False, "error": repr(exc)[:300]}
 
 
-def time_objectset(r, steps, warm, world, dev, dist, pipelined=None):
+def time_objectset(r, steps, warm, world, dev, dist, pipelined=True):
     """Time `steps` full passes of a RankRunner (every round: generate in HBM, seal, open, verify,
     digest; generate / verify overlapped with the crypt kernels of the neighbouring rounds unless
     pipelined=False) after `warm()`, bracketed by barrier + synchronize on both sides; counters
@@ -411,8 +411,6 @@ def time_objectset(r, steps, warm, world, dev, dist, pipelined=None):
     import torch
 
     from rclone_amd import shard
-    if pipelined is None:  # BENCH_OBJECTSET_PIPELINE=0: stream order (A/B)
-        pipelined = os.environ.get("BENCH_OBJECTSET_PIPELINE", "1") != "0"
     warm()
     torch.cuda.synchronize(dev)
     r.counters.zero_()
