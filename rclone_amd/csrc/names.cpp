@@ -678,16 +678,6 @@ struct SegBatch {
 
 // Host stages of a large batch run on up to kHostThreads threads, one chunk of names each.
 constexpr size_t kChunkNames = 8192;
-// Chunks per pipelined GPU group (rc_names_run): 256 k names; RCLONE_AMD_NAME_GROUP_CHUNKS
-// overrides (the sanitizer harness runs small batches through many groups).
-size_t group_chunks() {
-  static const size_t g = [] {
-    const char* v = getenv("RCLONE_AMD_NAME_GROUP_CHUNKS");
-    const long k = v ? atol(v) : 32;
-    return (size_t)(k > 0 ? k : 32);
-  }();
-  return g;
-}
 constexpr unsigned kHostThreads = 16;
 
 // A batch's host stages call parallel_for three or four times; spawning 16 threads each time
@@ -782,55 +772,37 @@ void parallel_for(size_t n, F f) {
   parallel_for_fn(n, std::function<void(size_t)>(f));
 }
 
-// One group of consecutive chunks shares an EME issue: its parts' segments packed into one
-// pinned slot of the name engine -> one H2D, one EME launch (in place), one D2H (names_gpu.cpp).
-// Issues are asynchronous, so the next group's host stages run while this one is on the GPU.
-struct GroupIo {
-  std::vector<size_t> base, dbase;  // each part's data / descriptor offset in the slot
-  size_t data_bytes = 0, ndesc = 0;
-};
-
-size_t group_descs(const std::vector<SegBatch*>& parts) {
-  size_t n = 0;
-  for (const auto* b : parts) n += b->desc.size();
-  return n;
-}
-
-int32_t eme_pack_issue(rcn::EmeDev* dev, int slot, const rc_cipher* c, bool encrypt, const std::vector<SegBatch*>& parts,
-                       GroupIo& io) {
-  const size_t nparts = parts.size();
-  io.base.assign(nparts + 1, 0);
-  io.dbase.assign(nparts + 1, 0);
+// All parts' segments in one pinned buffer -> one H2D, one EME launch (in place), one D2H
+// (names_gpu.cpp).
+int32_t run_eme(const rc_cipher* c, bool encrypt, std::vector<SegBatch*>& parts, double* ms) {
+  *ms = 0;
+  size_t nparts = parts.size();
+  std::vector<size_t> base(nparts + 1, 0), dbase(nparts + 1, 0);
   for (size_t i = 0; i < nparts; i++) {
-    io.base[i + 1] = io.base[i] + parts[i]->data.size();
-    io.dbase[i + 1] = io.dbase[i] + parts[i]->desc.size();
+    base[i + 1] = base[i] + parts[i]->data.size();
+    dbase[i + 1] = dbase[i] + parts[i]->desc.size();
   }
-  io.data_bytes = io.base[nparts];
-  io.ndesc = io.dbase[nparts];
-  if (io.ndesc == 0) return RC_NIL;
-  const size_t desc_off = (io.data_bytes + 255) & ~(size_t)255;
-  const size_t total = desc_off + io.ndesc * sizeof(xs_name_desc);
-  uint8_t* h = rcn::eme_slot(dev, slot, total);
-  if (!h) return RC_ERR_GPU;
+  const size_t data_bytes = base[nparts], ndesc = dbase[nparts];
+  if (ndesc == 0) return RC_NIL;
+  size_t desc_off = (data_bytes + 255) & ~(size_t)255;
+  size_t total = desc_off + ndesc * sizeof(xs_name_desc);
+  uint8_t* h = nullptr;
+  rcn::EmeDev* dev = rcn::eme_acquire(total, &h);
+  if (!dev) return RC_ERR_GPU;
   xs_name_desc* hd = (xs_name_desc*)(h + desc_off);
   parallel_for(nparts, [&](size_t i) {
     const SegBatch& b = *parts[i];
-    memcpy(h + io.base[i], b.data.data(), b.data.size());
+    memcpy(h + base[i], b.data.data(), b.data.size());
     for (size_t k = 0; k < b.desc.size(); k++) {
-      hd[io.dbase[i] + k] = b.desc[k];
-      hd[io.dbase[i] + k].off += io.base[i];
+      hd[dbase[i] + k] = b.desc[k];
+      hd[dbase[i] + k].off += base[i];
     }
   });
-  return rcn::eme_issue(dev, slot, encrypt, c, desc_off, io.ndesc, io.data_bytes, total);
-}
-
-int32_t eme_wait_unpack(rcn::EmeDev* dev, int slot, const std::vector<SegBatch*>& parts, const GroupIo& io, double* ms) {
-  if (io.ndesc == 0) return RC_NIL;
-  const int32_t rc = rcn::eme_wait(dev, slot, ms);
-  if (rc != RC_NIL) return rc;
-  const uint8_t* h = rcn::eme_slot(dev, slot, 0);
-  parallel_for(parts.size(), [&](size_t i) { memcpy(parts[i]->data.data(), h + io.base[i], parts[i]->data.size()); });
-  return RC_NIL;
+  int32_t rc = rcn::eme_run(dev, encrypt, c, desc_off, ndesc, data_bytes, total, ms);
+  if (rc == RC_NIL)
+    parallel_for(nparts, [&](size_t i) { memcpy(parts[i]->data.data(), h + base[i], parts[i]->data.size()); });
+  rcn::eme_release(dev);
+  return rc;
 }
 
 // ------------------------------------------------------------------ paths (flat, per chunk)
@@ -1146,92 +1118,46 @@ int32_t rc_names_run(rc_cipher* c, int32_t op, uint64_t n, const char* const* in
   rc_names* r = new rc_names();
   const size_t nchunks = (n + kChunkNames - 1) / kChunkNames;
   r->chunks.resize(nchunks);
-  // Groups of group_chunks() chunks go through the GPU one after another, pipelined: group g's
-  // host stages before the kernel (split, strip versions, pad / decode, pack) run while group
-  // g-1 is copied and transformed, and group g-1's stages after it (unpack, encode / unpad,
-  // first error per name, reassemble) while group g is.  Two staging slots alternate.
-  const size_t gch = group_chunks();
-  const size_t ngroups = (nchunks + gch - 1) / gch;
-  auto chunk_range = [&](size_t g, size_t* c0, size_t* c1) {
-    *c0 = g * gch;
-    *c1 = std::min(nchunks, *c0 + gch);
-  };
-  auto parts_of = [&](size_t g) {
-    size_t c0, c1;
-    chunk_range(g, &c0, &c1);
-    std::vector<SegBatch*> parts;
-    for (size_t ci = c0; ci < c1; ci++) parts.push_back(&r->chunks[ci].batch);
-    return parts;
-  };
-  auto prepare = [&](size_t g) {
-    size_t c0, c1;
-    chunk_range(g, &c0, &c1);
-    parallel_for(c1 - c0, [&](size_t k) {
-      const size_t ci = c0 + k;
-      Chunk& ch = r->chunks[ci];
-      uint64_t i0 = ci * kChunkNames, i1 = std::min<uint64_t>(n, i0 + kChunkNames);
-      ch.segs.reserve(i1 - i0);
-      ch.seg0.reserve(i1 - i0);
-      ch.direct.reserve(i1 - i0);
-      ch.roff.reserve(i1 - i0);
-      ch.rlen.reserve(i1 - i0);
-      ch.err.reserve(i1 - i0);
-      ch.batch.desc.reserve(i1 - i0);
-      ch.batch.data.reserve((i1 - i0) * 48);
-      for (uint64_t i = i0; i < i1; i++) prepare_input(x, ch, in[i], in_len[i]);
-    });
-  };
-  auto finish = [&](size_t g) {
-    size_t c0, c1;
-    chunk_range(g, &c0, &c1);
-    parallel_for(c1 - c0, [&](size_t k) {
-      const size_t ci = c0 + k;
-      Chunk& ch = r->chunks[ci];
-      uint64_t i0 = ci * kChunkNames, i1 = std::min<uint64_t>(n, i0 + kChunkNames);
-      ch.res.reserve(ch.res.size() + ch.batch.data.size() * 2 + (i1 - i0) * 8);
-      for (uint64_t i = i0; i < i1; i++) finish_input(x, ch, i - i0, in[i]);
-      std::vector<Seg>().swap(ch.segs);
-      std::vector<uint32_t>().swap(ch.seg0);
-      std::string().swap(ch.own);
-      std::string().swap(ch.segout);
-      ch.batch = SegBatch();
-    });
-  };
-  rcn::EmeDev* dev = nullptr;  // locked at the first group that needs the block cipher
-  std::vector<GroupIo> io(ngroups);
-  int32_t rc = RC_NIL;
-  double t_prep = 0, t_eme = 0, t_fin = 0;
-  for (size_t g = 0; g <= ngroups && rc == RC_NIL; g++) {
-    if (g < ngroups) {
-      auto t0 = std::chrono::steady_clock::now();
-      prepare(g);
-      t_prep += ms_since(t0);
-      t0 = std::chrono::steady_clock::now();
-      const auto parts = parts_of(g);
-      if (group_descs(parts) && !dev && !(dev = rcn::eme_open())) rc = RC_ERR_GPU;
-      if (rc == RC_NIL && dev) rc = eme_pack_issue(dev, (int)(g % 2), c, x.enc_dir, parts, io[g]);
-      t_eme += ms_since(t0);
-      if (rc != RC_NIL) break;
-    }
-    if (g >= 1) {
-      auto t0 = std::chrono::steady_clock::now();
-      if (dev) rc = eme_wait_unpack(dev, (int)((g - 1) % 2), parts_of(g - 1), io[g - 1], &r->kernel_ms);
-      t_eme += ms_since(t0);
-      if (rc != RC_NIL) break;
-      t0 = std::chrono::steady_clock::now();
-      finish(g - 1);
-      t_fin += ms_since(t0);
-    }
-  }
-  if (dev) rcn::eme_release(dev);  // waits for a group still in flight after an error
+  // host half before the kernel: split, strip versions, pad / decode, pack
+  parallel_for(nchunks, [&](size_t ci) {
+    Chunk& ch = r->chunks[ci];
+    uint64_t i0 = ci * kChunkNames, i1 = std::min<uint64_t>(n, i0 + kChunkNames);
+    ch.segs.reserve(i1 - i0);
+    ch.seg0.reserve(i1 - i0);
+    ch.direct.reserve(i1 - i0);
+    ch.roff.reserve(i1 - i0);
+    ch.rlen.reserve(i1 - i0);
+    ch.err.reserve(i1 - i0);
+    ch.batch.desc.reserve(i1 - i0);
+    ch.batch.data.reserve((i1 - i0) * 48);
+    for (uint64_t i = i0; i < i1; i++) prepare_input(x, ch, in[i], in_len[i]);
+  });
+  const double t_prep = ms_since(t_start);
+  std::vector<SegBatch*> parts(nchunks);
+  for (size_t ci = 0; ci < nchunks; ci++) parts[ci] = &r->chunks[ci].batch;
+  const auto t_eme0 = std::chrono::steady_clock::now();
+  int32_t rc = run_eme(c, x.enc_dir, parts, &r->kernel_ms);
+  const double t_eme = ms_since(t_eme0);
   if (rc != RC_NIL) {
     delete r;
     return rc;
   }
+  // host half after the kernel: encode / unpad, first error per name, reassemble
+  parallel_for(nchunks, [&](size_t ci) {
+    Chunk& ch = r->chunks[ci];
+    uint64_t i0 = ci * kChunkNames, i1 = std::min<uint64_t>(n, i0 + kChunkNames);
+    ch.res.reserve(ch.res.size() + ch.batch.data.size() * 2 + (i1 - i0) * 8);
+    for (uint64_t i = i0; i < i1; i++) finish_input(x, ch, i - i0, in[i]);
+    std::vector<Seg>().swap(ch.segs);
+    std::vector<uint32_t>().swap(ch.seg0);
+    std::string().swap(ch.own);
+    std::string().swap(ch.segout);
+    ch.batch = SegBatch();
+  });
   if (timing)
-    fprintf(stderr, "rc_names_run op %d n %llu: %.2f ms in %zu groups; host time in prepare %.2f ms, eme (pack + "
-            "issue + wait + unpack; kernels %.2f) %.2f ms, finish %.2f ms\n", (int)op, (unsigned long long)n,
-            ms_since(t_start), ngroups, t_prep, r->kernel_ms, t_eme, t_fin);
+    fprintf(stderr, "rc_names_run op %d n %llu: prepare %.2f ms, eme (pack + copies + kernel %.2f + unpack) %.2f ms, "
+            "finish %.2f ms\n", (int)op, (unsigned long long)n, t_prep, r->kernel_ms, t_eme,
+            ms_since(t_start) - t_prep - t_eme);
   *out = r;
   return RC_NIL;
 }

@@ -21,21 +21,16 @@ hipError_t launch_eme(bool encrypt, const aes::EmeKey& key, const xs_name_desc* 
 
 namespace rcn {
 
-struct EmeSlot {
-  uint8_t* d = nullptr;  // device
-  uint8_t* h = nullptr;  // pinned
-  size_t cap = 0;
-  hipEvent_t k0 = nullptr, k1 = nullptr;  // around the slot's kernel
-  hipEvent_t done = nullptr;              // after its D2H
-  bool pending = false;
-};
-
 struct EmeDev {
   std::mutex mu;
   bool init = false, failed = false;
   int device = 0;
   hipStream_t s = nullptr;
-  EmeSlot slot[2];
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  uint8_t* d_buf = nullptr;
+  size_t d_cap = 0;
+  uint8_t* h_buf = nullptr;  // pinned
+  size_t h_cap = 0;
 };
 
 namespace {
@@ -66,11 +61,8 @@ EmeDev& name_engine() {
 bool ne_init(EmeDev& e) {
   if (e.init) return true;
   if (e.failed) return false;
-  bool ok = hipSetDevice(e.device) == hipSuccess && hipStreamCreateWithFlags(&e.s, hipStreamNonBlocking) == hipSuccess;
-  for (auto& sl : e.slot)
-    ok = ok && hipEventCreate(&sl.k0) == hipSuccess && hipEventCreate(&sl.k1) == hipSuccess &&
-         hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
-  if (!ok) {
+  if (hipSetDevice(e.device) != hipSuccess || hipStreamCreateWithFlags(&e.s, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&e.ev0) != hipSuccess || hipEventCreate(&e.ev1) != hipSuccess) {
     xs::set_error("name engine: no HIP device %d", e.device);
     e.failed = true;
     return false;
@@ -79,77 +71,56 @@ bool ne_init(EmeDev& e) {
   return true;
 }
 
+bool ne_reserve(EmeDev& e, size_t bytes) {
+  if (bytes <= e.d_cap && bytes <= e.h_cap) return true;
+  size_t cap = e.d_cap ? e.d_cap : (1u << 20);
+  while (cap < bytes) cap *= 2;
+  if (e.d_buf) (void)hipFree(e.d_buf);
+  if (e.h_buf) (void)hipHostFree(e.h_buf);
+  e.d_buf = e.h_buf = nullptr;
+  e.d_cap = e.h_cap = 0;
+  if (hipMalloc(&e.d_buf, cap) != hipSuccess || hipHostMalloc(&e.h_buf, cap, hipHostMallocPortable) != hipSuccess) {
+    xs::set_error("name engine: cannot allocate %zu bytes", cap);
+    return false;
+  }
+  e.d_cap = e.h_cap = cap;
+  return true;
+}
+
 }  // namespace
 
-EmeDev* eme_open() {
+EmeDev* eme_acquire(size_t bytes, uint8_t** host) {
   EmeDev& e = name_engine();
   e.mu.lock();
-  if (!ne_init(e) || hipSetDevice(e.device) != hipSuccess) {
+  if (!ne_init(e) || hipSetDevice(e.device) != hipSuccess || !ne_reserve(e, bytes)) {
     e.mu.unlock();
     return nullptr;
   }
+  *host = e.h_buf;
   return &e;
 }
 
-uint8_t* eme_slot(EmeDev* dev, int s, size_t bytes) {
-  EmeSlot& sl = dev->slot[s];
-  if (bytes <= sl.cap) return sl.h;
-  size_t cap = sl.cap ? sl.cap : (1u << 20);
-  while (cap < bytes) cap *= 2;
-  if (sl.d) (void)hipFree(sl.d);
-  if (sl.h) (void)hipHostFree(sl.h);
-  sl.d = sl.h = nullptr;
-  sl.cap = 0;
-  if (hipMalloc(&sl.d, cap) != hipSuccess || hipHostMalloc(&sl.h, cap, hipHostMallocPortable) != hipSuccess) {
-    xs::set_error("name engine: cannot allocate %zu bytes", cap);
-    return nullptr;
-  }
-  sl.cap = cap;
-  return sl.h;
-}
-
-int32_t eme_issue(EmeDev* dev, int s, bool encrypt, const rc_cipher* c, size_t desc_off, size_t ndesc,
-                  size_t data_bytes, size_t total) {
+int32_t eme_run(EmeDev* dev, bool encrypt, const rc_cipher* c, size_t desc_off, size_t ndesc, size_t data_bytes,
+                size_t total, double* ms) {
   EmeDev& e = *dev;
-  EmeSlot& sl = e.slot[s];
-  hipError_t err = hipMemcpyAsync(sl.d, sl.h, total, hipMemcpyHostToDevice, e.s);
-  if (err == hipSuccess) err = hipEventRecord(sl.k0, e.s);
+  hipError_t err = hipMemcpyAsync(e.d_buf, e.h_buf, total, hipMemcpyHostToDevice, e.s);
+  if (err == hipSuccess) err = hipEventRecord(e.ev0, e.s);
   if (err == hipSuccess)
-    err = xs::launch_eme(encrypt, c->eme, (const xs_name_desc*)(sl.d + desc_off), ndesc, sl.d, sl.d, data_bytes, e.s);
-  if (err == hipSuccess) err = hipEventRecord(sl.k1, e.s);
-  if (err == hipSuccess) err = hipMemcpyAsync(sl.h, sl.d, data_bytes, hipMemcpyDeviceToHost, e.s);
-  if (err == hipSuccess) err = hipEventRecord(sl.done, e.s);
-  sl.pending = true;  // waited for even after a failed issue: earlier work may be queued
-  if (err != hipSuccess) {
-    xs::set_error("name engine: %s", hipGetErrorString(err));
-    return RC_ERR_GPU;
-  }
-  return RC_NIL;
-}
-
-int32_t eme_wait(EmeDev* dev, int s, double* ms) {
-  EmeDev& e = *dev;
-  EmeSlot& sl = e.slot[s];
-  if (!sl.pending) return RC_NIL;
-  sl.pending = false;
-  hipError_t err = hipEventSynchronize(sl.done);
-  if (err != hipSuccess) err = hipStreamSynchronize(e.s);
+    err = xs::launch_eme(encrypt, c->eme, (const xs_name_desc*)(e.d_buf + desc_off), ndesc, e.d_buf, e.d_buf,
+                         data_bytes, e.s);
+  if (err == hipSuccess) err = hipEventRecord(e.ev1, e.s);
+  if (err == hipSuccess) err = hipMemcpyAsync(e.h_buf, e.d_buf, data_bytes, hipMemcpyDeviceToHost, e.s);
+  if (err == hipSuccess) err = hipStreamSynchronize(e.s);
   if (err != hipSuccess) {
     xs::set_error("name engine: %s", hipGetErrorString(err));
     return RC_ERR_GPU;
   }
   float f = 0;
-  if (hipEventElapsedTime(&f, sl.k0, sl.k1) == hipSuccess) *ms += f;
+  if (hipEventElapsedTime(&f, e.ev0, e.ev1) == hipSuccess) *ms = f;
   return RC_NIL;
 }
 
-void eme_release(EmeDev* dev) {
-  for (int s = 0; s < 2; s++) {
-    double ms = 0;
-    (void)eme_wait(dev, s, &ms);  // nothing may still write a slot once another call owns it
-  }
-  dev->mu.unlock();
-}
+void eme_release(EmeDev* dev) { dev->mu.unlock(); }
 
 }  // namespace rcn
 

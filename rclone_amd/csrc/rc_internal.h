@@ -36,20 +36,13 @@ struct rc_cipher {
   std::mutex rand_mu;
 };
 
-// The name cipher's GPU side (names_gpu.cpp), called by the host half (names.cpp).  An engine is
-// locked for one rc_names_run call and has two staging slots (pinned host + device buffer), so the
-// host stages of one group of names overlap the copies and kernel of the previous group.
+// The name cipher's GPU side (names_gpu.cpp), called by the host half (names.cpp).
 namespace rcn {
 struct EmeDev;
-// Lock a name engine (nullptr with xs_last_error when there is no device).
-EmeDev* eme_open();
-// Slot s's pinned staging, grown to >= bytes (the slot must be idle: waited for, or never issued).
-uint8_t* eme_slot(EmeDev* dev, int s, size_t bytes);
-// Asynchronously: slot s's host[0:total] -> device, EME in place over the names (descriptors at
-// desc_off), data_bytes back into host.  One stream per engine: issues complete in order.
-int32_t eme_issue(EmeDev* dev, int s, bool encrypt, const rc_cipher* c, size_t desc_off, size_t ndesc,
-                  size_t data_bytes, size_t total);
-// Wait for slot s's issue (no-op if none); *ms += its kernel time.
-int32_t eme_wait(EmeDev* dev, int s, double* ms);
+// Lock a name engine whose pinned staging holds >= bytes; *host = that staging (nullptr on error).
+EmeDev* eme_acquire(size_t bytes, uint8_t** host);
+// host[0:total] -> device, EME in place over the names (descriptors at desc_off), data back.
+int32_t eme_run(EmeDev* dev, bool encrypt, const rc_cipher* c, size_t desc_off, size_t ndesc, size_t data_bytes,
+                size_t total, double* ms);
 void eme_release(EmeDev* dev);
 }  // namespace rcn

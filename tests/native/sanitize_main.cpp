@@ -908,7 +908,6 @@ static void test_concurrency(rc_cipher* c, const uint8_t key[32]) {
 int main(int argc, char** argv) {
   const bool only_concurrency = argc > 1 && !strcmp(argv[1], "--concurrency");
   setenv("RCLONE_AMD_NAME_THREADS", "16", 1);
-  setenv("RCLONE_AMD_NAME_GROUP_CHUNKS", "1", 0);  // every 8192-name chunk its own pipelined group
   int32_t err = 0;
   rc_cipher* c = rc_cipher_new("potato", "", &err);
   if (!c) {

@@ -149,45 +149,30 @@ int xs_pool_seal_md5(xs_pool*, const uint8_t key[32], uint64_t nobj, const uint8
 namespace rcn {
 struct EmeDev {
   std::mutex mu;
-  std::vector<uint8_t> h[2];
-  bool pending[2] = {false, false};
+  std::vector<uint8_t> h;
 };
 static EmeDev g_dev;
 
-EmeDev* eme_open() {
+EmeDev* eme_acquire(size_t bytes, uint8_t** host) {
   g_dev.mu.lock();
+  if (g_dev.h.size() < bytes) g_dev.h.resize(bytes);
+  *host = g_dev.h.data();
   return &g_dev;
 }
 
-uint8_t* eme_slot(EmeDev* dev, int s, size_t bytes) {
-  if (dev->pending[s]) abort();  // a slot is only refilled after its issue was waited for
-  if (dev->h[s].size() < bytes) dev->h[s].resize(bytes);
-  return dev->h[s].data();
-}
-
-// the oracle transforms the slot at issue time; the wait only checks the protocol
-int32_t eme_issue(EmeDev* dev, int s, bool encrypt, const rc_cipher* c, size_t desc_off, size_t ndesc,
-                  size_t data_bytes, size_t total) {
-  if (dev->pending[s] || total > dev->h[s].size()) abort();
-  const xs_name_desc* d = (const xs_name_desc*)(dev->h[s].data() + desc_off);
+int32_t eme_run(EmeDev* dev, bool encrypt, const rc_cipher* c, size_t desc_off, size_t ndesc, size_t data_bytes,
+                size_t total, double* ms) {
+  const xs_name_desc* d = (const xs_name_desc*)(dev->h.data() + desc_off);
   for (size_t i = 0; i < ndesc; i++) {
     if (d[i].off + 16ull * d[i].nblk > data_bytes || d[i].nblk < 1 || d[i].nblk > 128 || total < desc_off) abort();
-    uint8_t* p = dev->h[s].data() + d[i].off;
+    uint8_t* p = dev->h.data() + d[i].off;
     std::vector<uint8_t> out(16 * d[i].nblk);
     if (orc_eme_transform(c->name_key, c->name_tweak, p, out.data(), (int)d[i].nblk, encrypt ? 0 : 1) != 0) abort();
     memcpy(p, out.data(), out.size());
   }
-  dev->pending[s] = true;
+  *ms = 0;
   return RC_NIL;
 }
 
-int32_t eme_wait(EmeDev* dev, int s, double*) {
-  dev->pending[s] = false;
-  return RC_NIL;
-}
-
-void eme_release(EmeDev* dev) {
-  dev->pending[0] = dev->pending[1] = false;
-  dev->mu.unlock();
-}
+void eme_release(EmeDev* dev) { dev->mu.unlock(); }
 }  // namespace rcn
