@@ -402,12 +402,10 @@ def _pool_check_body(devices):
         return {"devices": n_dev, "ran": True, "ok": False, "error": repr(exc)[:300]}
 
 
-def time_objectset(r, steps, warm, world, dev, dist, pipelined=True):
+def time_objectset(r, steps, warm, world, dev, dist):
     """Time `steps` full passes of a RankRunner (every round: generate in HBM, seal, open, verify,
-    digest; generate / verify overlapped with the crypt kernels of the neighbouring rounds unless
-    pipelined=False) after `warm()`, bracketed by barrier + synchronize on both sides; counters
-    summed and the time max-reduced over the ranks.  Returns (seconds, summed counters, kernel ms
-    lists)."""
+    digest) after `warm()`, bracketed by barrier + synchronize on both sides; counters summed and
+    the time max-reduced over the ranks.  Returns (seconds, summed counters, kernel ms lists)."""
     import torch
 
     from rclone_amd import shard
@@ -420,7 +418,7 @@ def time_objectset(r, steps, warm, world, dev, dist, pipelined=True):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
-        (r.run_all_pipelined if pipelined else r.run_all)(record=True)
+        r.run_all(record=True)
     torch.cuda.synchronize(dev)
     if grouped(world):
         dist.barrier()
@@ -453,7 +451,7 @@ def objectset_leg(args, world, rank, dev, dist):
 
     def warm():
         for _ in range(args.objectset_warmup):
-            r.run_all_pipelined()
+            r.run_all()
     el, counters, seal_ms, open_ms = time_objectset(r, args.objectset_steps, warm, world, dev, dist)
     blocks, nbytes, fails, mism, d0, d1 = digest_to_u64(counters)
     digest = f"{d1:016x}{d0:016x}"  # the last pass's, summed over the ranks
@@ -465,8 +463,7 @@ def objectset_leg(args, world, rank, dev, dist):
         return None
     return {"workload": f"BASELINE configs[3]: one {total}-block object ({total * BLOCK_DATA / 2**40:.3f} TiB) "
                         f"round-robin over {world} rank(s), {CONFIG3_ROUND_BLOCKS}-block rounds; one step = "
-                        "generate in HBM + seal + open + verify every block (generate / verify of "
-                        "neighbouring rounds overlapped with seal / open on a second stream)",
+                        "generate in HBM + seal + open + verify every block",
             "value": round(2 * nbytes / 2**30 / el, 3), "unit": "GiB/s", "scaling": "strong",
             "steps": args.objectset_steps, "warmup": args.objectset_warmup,
             "ms_per_step": round(el / args.objectset_steps * 1e3, 3), "ok": ok,
@@ -485,8 +482,6 @@ def run_objectset(args, world, rank, dev, dist):
     --blocks rounds; one step = every round (generate in HBM, seal, open, verify, digest)."""
     from rclone_amd.objectset import CONFIG3_KEY, CONFIG3_NONCE0, CONFIG3_SEED, RankRunner, digest_to_u64
     r = RankRunner(CONFIG3_KEY, CONFIG3_NONCE0, args.object_blocks, world, rank, args.blocks, CONFIG3_SEED, dev)
-
-    r.prepare_pipeline()
 
     def warm():
         for _ in range(args.warmup):

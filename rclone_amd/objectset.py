@@ -76,56 +76,37 @@ class RankRunner:
         self.ws_open = device.workspace(B, self.dev)
         self.counters = torch.zeros(N_COUNTERS, dtype=torch.int64, device=self.dev)
         self.kernel_events = []  # (seal?, start, end) around every crypt launch when timing
-        self._pipe = None  # second buffer set + streams of run_all_pipelined, made on first use
-
-    def _span(self, k: int):
-        lo = k * self.B
-        nb = min(self.B, self.n - lo)
-        return lo, nb, nb * BLOCK_DATA, nb * BLOCK_SIZE
-
-    def _fill(self, k: int, plain: torch.Tensor):
-        # global blocks gidx[lo:lo+nb] = rank + world*(lo..): first gidx[lo], stride world
-        lo, _, plen, _ = self._span(k)
-        device.fill_blocks(plain[:plen], int(self.gidx[lo]), self.world, self.seed)
-
-    def _verify(self, k: int, out: torch.Tensor, mismatch: torch.Tensor):
-        # opened plaintext vs the generator's stream, recomputed (the kept plaintext is not re-read)
-        lo, _, plen, _ = self._span(k)
-        device.verify_blocks(out[:plen], int(self.gidx[lo]), self.world, self.seed, mismatch)
-
-    def _crypt(self, k: int, bufs, stream, record: bool):
-        """Key schedules, seal, open, verdict count and tag digest of round k on `stream`."""
-        plain, body, out, ok, ws_seal, ws_open = bufs
-        L = _lib.lib()
-        sp = ctypes.c_void_p(stream.cuda_stream)
-        lo, nb, plen, blen = self._span(k)
-        ds = self.d_seal[lo * 48:(lo + nb) * 48]
-        do = self.d_open[lo * 48:(lo + nb) * 48]
-        _lib.check(L.xs_keygen_batch_dev(1, self.key, ds.data_ptr(), nb, plain.data_ptr(), plen,
-                                         body.data_ptr(), blen, ws_seal.data_ptr(), sp), "keygen")
-        ev = self._ev(record, stream)
-        _lib.check(L.xs_crypt_dev(1, ws_seal.data_ptr(), nb, plain.data_ptr(), body.data_ptr(), None, sp), "seal")
-        self._ev_end(ev, True, stream)
-        _lib.check(L.xs_keygen_batch_dev(0, self.key, do.data_ptr(), nb, body.data_ptr(), blen,
-                                         out.data_ptr(), plen, ws_open.data_ptr(), sp), "keygen")
-        ev = self._ev(record, stream)
-        _lib.check(L.xs_crypt_dev(0, ws_open.data_ptr(), nb, body.data_ptr(), out.data_ptr(), ok.data_ptr(), sp),
-                   "open")
-        self._ev_end(ev, False, stream)
-        with torch.cuda.stream(stream):
-            c = self.counters
-            c[0] += nb
-            c[1] += plen
-            c[2] += nb - ok[:nb].sum(dtype=torch.int64)
-            c[4:6] += tag_digest(body, nb)
 
     def run_round(self, k: int, record: bool = False):
-        """Round k in stream order on the current stream: generate, seal, open, verify."""
+        L = _lib.lib()
         stream = torch.cuda.current_stream(self.dev)
-        bufs = (self.plain, self.body, self.out, self.ok, self.ws_seal, self.ws_open)
-        self._fill(k, self.plain)
-        self._crypt(k, bufs, stream, record)
-        self._verify(k, self.out, self.counters[3:4])
+        sp = ctypes.c_void_p(stream.cuda_stream)
+        lo = k * self.B
+        nb = min(self.B, self.n - lo)
+        plen, blen = nb * BLOCK_DATA, nb * BLOCK_SIZE
+        # global blocks gidx[lo:lo+nb] = rank + world*(lo..): first gidx[lo], stride world
+        device.fill_blocks(self.plain[:plen], int(self.gidx[lo]), self.world, self.seed)
+        ds = self.d_seal[lo * 48:(lo + nb) * 48]
+        do = self.d_open[lo * 48:(lo + nb) * 48]
+        _lib.check(L.xs_keygen_batch_dev(1, self.key, ds.data_ptr(), nb, self.plain.data_ptr(), plen,
+                                         self.body.data_ptr(), blen, self.ws_seal.data_ptr(), sp), "keygen")
+        ev = self._ev(record, stream)
+        _lib.check(L.xs_crypt_dev(1, self.ws_seal.data_ptr(), nb, self.plain.data_ptr(), self.body.data_ptr(),
+                                  None, sp), "seal")
+        self._ev_end(ev, True, stream)
+        _lib.check(L.xs_keygen_batch_dev(0, self.key, do.data_ptr(), nb, self.body.data_ptr(), blen,
+                                         self.out.data_ptr(), plen, self.ws_open.data_ptr(), sp), "keygen")
+        ev = self._ev(record, stream)
+        _lib.check(L.xs_crypt_dev(0, self.ws_open.data_ptr(), nb, self.body.data_ptr(), self.out.data_ptr(),
+                                  self.ok.data_ptr(), sp), "open")
+        self._ev_end(ev, False, stream)
+        c = self.counters
+        c[0] += nb
+        c[1] += plen
+        c[2] += nb - self.ok[:nb].sum(dtype=torch.int64)
+        # opened plaintext vs the generator's stream, recomputed (the kept plaintext is not re-read)
+        device.verify_blocks(self.out[:plen], int(self.gidx[lo]), self.world, self.seed, c[3:4])
+        c[4:6] += tag_digest(self.body, nb)
 
     def _ev(self, record, stream):
         if not record:
@@ -148,68 +129,6 @@ class RankRunner:
         self.counters[4:6].zero_()
         for k in range(self.rounds):
             self.run_round(k, record)
-        return self.counters
-
-    def prepare_pipeline(self):
-        """Allocate run_all_pipelined's second buffer set and its two streams (once)."""
-        if self._pipe is None:
-            B = self.B
-            second = (torch.empty(B * BLOCK_DATA, dtype=torch.uint8, device=self.dev),
-                      torch.empty(B * BLOCK_SIZE, dtype=torch.uint8, device=self.dev),
-                      torch.empty(B * BLOCK_DATA, dtype=torch.uint8, device=self.dev),
-                      torch.empty(B, dtype=torch.uint8, device=self.dev),
-                      device.workspace(B, self.dev), device.workspace(B, self.dev))
-            self._pipe = {"bufs": [(self.plain, self.body, self.out, self.ok, self.ws_seal, self.ws_open), second],
-                          "crypt": torch.cuda.Stream(self.dev), "data": torch.cuda.Stream(self.dev),
-                          "mismatch": torch.zeros(1, dtype=torch.int64, device=self.dev)}
-
-    def run_all_pipelined(self, record: bool = False):
-        """The same pass, with the memory-bound generate / verify kernels of neighbouring rounds
-        overlapped with the VALU-bound seal / open kernels: two buffer sets, the crypt work of
-        round k on one stream while another generates round k+1 (or k+2) and verifies round k-1.
-        Same bytes, counters and digest as run_all (tests/test_objectset_gpu.py); the caller's
-        current stream is joined on entry and waits for both streams on exit."""
-        self.prepare_pipeline()
-        P = self._pipe
-        s_c, s_d, bufs, mism = P["crypt"], P["data"], P["bufs"], P["mismatch"]
-        cur = torch.cuda.current_stream(self.dev)
-        self.counters[4:6].zero_()
-        mism.zero_()
-        s_c.wait_stream(cur)
-        s_d.wait_stream(cur)
-        R = self.rounds
-        ev_fill, ev_crypt, ev_ver = [None] * R, [None] * R, [None] * R
-
-        def mark(stream):
-            e = torch.cuda.Event()
-            e.record(stream)
-            return e
-
-        def fill(k):
-            with torch.cuda.stream(s_d):
-                if k >= 2:
-                    s_d.wait_event(ev_crypt[k - 2])  # round k-2's seal has read this plaintext buffer
-                self._fill(k, bufs[k % 2][0])
-                ev_fill[k] = mark(s_d)
-
-        fill(0)
-        if R > 1:
-            fill(1)
-        for k in range(R):
-            s_c.wait_event(ev_fill[k])
-            if k >= 2:
-                s_c.wait_event(ev_ver[k - 2])  # round k-2's output buffer has been verified
-            self._crypt(k, bufs[k % 2], s_c, record)
-            ev_crypt[k] = mark(s_c)
-            with torch.cuda.stream(s_d):
-                s_d.wait_event(ev_crypt[k])
-                self._verify(k, bufs[k % 2][2], mism)
-                ev_ver[k] = mark(s_d)
-            if k + 2 < R:
-                fill(k + 2)
-        cur.wait_stream(s_c)
-        cur.wait_stream(s_d)
-        self.counters[3:4] += mism
         return self.counters
 
     def block(self, g: int):
