@@ -11,10 +11,14 @@ object set; no payload crosses ranks).  Counters (blocks, bytes, tag failures) a
 across ranks with one RCCL all-reduce after the timed region.
 
 Also reported: the dominant kernel's roofline (HBM; achieved algorithmic GB/s from HIP events
-around every xs_crypt launch inside the timed region) and the CPU baseline (the oracle's
-C restatement, OpenMP, on this host's cores, bounded sample) -- see DESIGN.md.
+around every xs_crypt launch inside the timed region), the CPU baseline (the oracle's
+C restatement, OpenMP, on this host's cores, bounded sample), and -- after the headline timing,
+outside it -- BASELINE configs[3] as the `objectset` key: a 1 TiB object round-robin over the N
+ranks (fixed total work: strong scaling), generated, sealed, opened and verified, with a tag
+digest that must equal the one-GPU digest (rclone_amd.objectset.CONFIG3_TAG_DIGEST) -- see
+DESIGN.md.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--blocks B] [--no-cpu]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--blocks B] [--no-cpu] [--objectset-steps S]
 """
 import argparse
 import ctypes
