@@ -32,6 +32,9 @@ def need_gpu():
 def _bench(*args, gloo=True, env_extra=None):
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "BENCH_FORCE_PG")}
+    # the default mode's configs[3] leg over a 400 000-block object instead of 1 TiB (one step):
+    # the same code, the same cross-rank sums, seconds instead of tens of seconds
+    env["BENCH_OBJECTSET_BLOCKS"] = "400000"
     if gloo:
         env["BENCH_DIST_BACKEND"] = "gloo"
     env.update(env_extra or {})
@@ -45,8 +48,8 @@ def _bench(*args, gloo=True, env_extra=None):
 
 def test_bench_two_ranks_default_mode_matches_one_rank():
     nb = 8192
-    two = _bench("--gpus", "2", "--steps", "2", "--warmup", "1", "--blocks", str(nb))
-    one = _bench("--gpus", "1", "--steps", "2", "--warmup", "1", "--blocks", str(2 * nb))
+    two = _bench("--gpus", "2", "--steps", "2", "--warmup", "1", "--blocks", str(nb), "--objectset-steps", "1")
+    one = _bench("--gpus", "1", "--steps", "2", "--warmup", "1", "--blocks", str(2 * nb), "--objectset-steps", "1")
     assert two["n_gpus"] == 2 and two["config"]["ranks_seen"] == 2 and len(two["config"]["rank_gpus"]) == 2
     assert two["config"]["distinct_gpus"] == min(2, torch.cuda.device_count())
     # counters summed over the ranks: 2 ranks x 2 steps x (seal + open) x nb blocks
@@ -56,6 +59,11 @@ def test_bench_two_ranks_default_mode_matches_one_rank():
     assert two["counters"]["tag_digest"] == one["counters"]["tag_digest"]
     assert two["build_id"] == one["build_id"]
     assert two["value"] > 0 and two["scaling"] == "weak"
+    # the configs[3] leg: a fixed object split over the ranks, the same digest for 1 and 2 ranks
+    for k in ("blocks", "bytes", "tag_failures", "roundtrip_mismatch_words", "tag_digest"):
+        assert two["objectset"]["counters"][k] == one["objectset"]["counters"][k], k
+    assert two["objectset"]["ok"] and one["objectset"]["ok"] and two["objectset"]["scaling"] == "strong"
+    assert two["objectset"]["counters"]["blocks"] == 400000
 
 
 def test_bench_two_ranks_object_set_matches_one_rank():
@@ -80,7 +88,7 @@ def test_bench_rccl_one_rank_group_matches_no_group():
     the counter SUM and the time MAX all-reduces, destroy), run for real on this box's GPU through
     a one-rank RCCL group (BENCH_FORCE_PG=1; two RCCL ranks cannot share one device), in each
     mode: the results equal the run without a group."""
-    base = ["--gpus", "1", "--steps", "2", "--warmup", "1"]
+    base = ["--gpus", "1", "--steps", "2", "--warmup", "1", "--objectset-steps", "1"]
     for extra in (["--blocks", "8192"], ["--object-blocks", "40000", "--blocks", "8192"], ["--names", "20000"],
                   ["--mixed-gib", "0.1"]):
         pg = _bench(*base, *extra, gloo=False, env_extra={"BENCH_FORCE_PG": "1", "BENCH_DIST_BACKEND": "nccl"})
@@ -95,6 +103,8 @@ def test_bench_rccl_one_rank_group_matches_no_group():
             continue
         for k in ("blocks", "bytes", "tag_failures", "tag_digest"):
             assert pg["counters"][k] == one["counters"][k], (extra, k)
+        if pg.get("objectset"):  # the default mode's configs[3] leg through the RCCL group
+            assert pg["objectset"]["counters"]["tag_digest"] == one["objectset"]["counters"]["tag_digest"]
 
 
 def test_bench_rccl_refuses_more_ranks_than_gpus():
