@@ -392,7 +392,14 @@ static void test_readahead(rc_cipher* c) {
     CHECK(s.pos == 65536, "first data byte read %zu source bytes", s.pos);
     rc_encrypter_read(e, buf.data(), 65535 + 16, &err);
     rc_encrypter_read(e, buf.data(), 1, &err);
-    CHECK(s.pos == (growth == 2 ? 3u : 17u) * 65536, "growth %u: second refill ends at %zu", growth, s.pos);
+    // growth 0 jumps to full batches only after a refill read faster than 2 GB/s: a memory source
+    // is that fast, except under ThreadSanitizer's instrumentation, where it may double instead
+#if defined(__SANITIZE_THREAD__)
+    const bool slow_ok = growth == 0 && s.pos == 3u * 65536;
+#else
+    const bool slow_ok = false;
+#endif
+    CHECK(s.pos == (growth == 2 ? 3u : 17u) * 65536 || slow_ok, "growth %u: second refill ends at %zu", growth, s.pos);
     rc_encrypter_free(e);
   }
   rc_cipher_set_batch_blocks(c, 64);

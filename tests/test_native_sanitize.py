@@ -9,7 +9,8 @@
   ThreadSanitizer, with the GPU side replaced by the CPU oracle (tests/native/stub_engine.cpp,
   test-only): stream round trips, truncation / bit-flip / reader-error fuzz with exact error
   positions, a seek/limit grid, name decoders and DecryptFileName on garbage, and concurrent
-  streams plus a 16-thread names batch (the reference runs `go test -race`, Makefile:103-104).
+  streams plus a 16-thread names batch, all under TSan too (the reference runs `go test -race`,
+  Makefile:103-104).
 """
 import os
 import subprocess
@@ -59,6 +60,9 @@ def test_host_cpp_asan_ubsan(built):
     assert int(out.split("(")[1].split()[0]) > 10000
 
 
-def test_host_cpp_tsan_concurrency(built):
-    out = run(os.path.join(built, "sanitize_tsan"), "--concurrency")
+def test_host_cpp_tsan(built):
+    # every harness check under ThreadSanitizer (concurrent streams, the 16-thread names batch, the
+    # MD5 worker tiers, and the single-threaded checks whose code paths those share)
+    out = run(os.path.join(built, "sanitize_tsan"), timeout=900)
     assert "sanitize ok" in out
+    assert int(out.split("(")[1].split()[0]) > 10000
