@@ -271,3 +271,16 @@ def test_reopen_error_keeps_the_openers_error():
     assert "couldn't reopen file with offset and limit: object not found" in str(ei.value)
     assert isinstance(ei.value.__cause__, Gone)
     assert calls == [(0, 32), (32 + 65552, -1)]
+
+
+def test_ablation_patches_still_apply():
+    """tools/ablate_variant.py keeps the diagnostic (wrong-output) kernel variants out of the
+    product file as text patches; their anchors must follow the product kernel or they rot."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ablate_variant", os.path.join(ROOT, "tools", "ablate_variant.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    src = open(mod.SRC).read()
+    for name in mod.PATCHES:
+        patched = mod.variant_source(name)  # raises SystemExit when an anchor is missing
+        assert patched != src, name
