@@ -11,13 +11,19 @@
  *   gpucipher_compute_hash  -> computeHashWithNonce                  (crypt.go:784-806)
  *   gpucipher_hash_batch    -> the same, batched                     (cmd/cryptcheck/cryptcheck.go:67-117)
  *
- * Usage: c_client_gpu <manifest>.  Manifest line 1: the data key (64 hex digits); then one case
- * per line: "<nonce hex> <plaintext path> <crypt file out path>".  For each case the client
- * writes the crypt file the encrypter produced (the test compares it with the reference's /
+ * Usage: c_client_gpu <manifest> [threads].  Manifest line 1: the data key (64 hex digits); then
+ * one case per line: "<nonce hex> <plaintext path> <crypt file out path>".  For each case the
+ * client writes the crypt file the encrypter produced (the test compares it with the reference's /
  * libsodium's fixture) and checks on its own that decrypting it, seeking into it and reading a
  * tampered copy behave as cipher.go does.  It prints one line per case:
- *   case <i> size <n> tee <md5> hash <md5> batch <md5> bad_block_at <bytes> opens <n>
- * and "c client gpu ok" last when every check passed. */
+ *   case <i> size <n> tee <md5> hash <md5> bad_block_at <bytes> opens <n>
+ * then "batch <i> <md5>" per case, and "c client gpu ok" last when every check passed.
+ * With threads > 1, that many threads run every case at once over the one shared cipher -- the
+ * Go side's --transfers / --checkers goroutines calling through the shim concurrently, so the
+ * engine coalesces their blocks into shared launches -- and every thread's crypt bytes, tee,
+ * hash and batch digests must equal thread 0's (which are the ones printed and written). */
+#include <pthread.h>
+#include <stdatomic.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -36,7 +42,7 @@ int32_t gpucipher_compute_hash(rc_cipher *c, uintptr_t src, int closer, const ui
 int32_t gpucipher_hash_batch(rc_cipher *c, uint64_t n, const uintptr_t *srcs, uint64_t n_nonces, const uint8_t *nonces,
                              uint8_t *md5, int32_t *errs);
 
-static int failures = 0;
+static atomic_int failures;
 #define CHECK(c, ...)                   \
   do {                                  \
     if (!(c)) {                         \
@@ -47,8 +53,8 @@ static int failures = 0;
     }                                   \
   } while (0)
 
-/* ---- the "Go side": handles 1.. are readers (runtime/cgo.Handle values), OPENER_BASE + i the
- * OpenRangeSeek of case i's crypt file (gpucipher.go goOpen).  Readers hand out at most `chunk`
+/* ---- the "Go side": handles 1.. are readers (runtime/cgo.Handle values), OPENER_BASE +
+ * MAXCASE * t + i the OpenRangeSeek of thread t's crypt file of case i (gpucipher.go goOpen).  Readers hand out at most `chunk`
  * bytes per Read, like a socket does: the library's ReadFill must gather whole blocks itself. */
 typedef struct {
   const uint8_t *p;
@@ -58,18 +64,19 @@ typedef struct {
   int32_t fail;  /* returned once pos == end (RC_EOF for a clean end) */
   int reads, closes, seeks;
 } box;
-#define MAXBOX 512
-#define OPENER_BASE 100000u
+#define MAXBOX 16384
+#define OPENER_BASE 1000000u
 static box boxes[MAXBOX];
-static int nbox = 1; /* handle 0 unused: a cgo.Handle is never 0 */
+static atomic_int nbox = 1; /* handle 0 unused: a cgo.Handle is never 0 */
 
 static uintptr_t new_box(const uint8_t *p, int64_t pos, int64_t end, int64_t full, int64_t chunk) {
-  if (nbox >= MAXBOX) {
+  const int h = atomic_fetch_add(&nbox, 1);
+  if (h >= MAXBOX) {
     fprintf(stderr, "handle table full\n");
     exit(2);
   }
-  boxes[nbox] = (box){p, end, pos, full, chunk, RC_EOF, 0, 0, 0};
-  return (uintptr_t)nbox++;
+  boxes[h] = (box){p, end, pos, full, chunk, RC_EOF, 0, 0, 0};
+  return (uintptr_t)h;
 }
 
 int64_t goRead(uintptr_t h, uint8_t *p, int64_t n, int32_t *err) {
@@ -88,15 +95,23 @@ int32_t goClose(uintptr_t h) {
   return RC_NIL;
 }
 
-/* crypt files of the cases, served by the openers */
+/* the cases (read-only once loaded) and each thread's results, its crypt files served by the openers */
 typedef struct {
-  uint8_t *plain, *crypt;
-  int64_t plain_n, crypt_n;
+  uint8_t *plain;
+  int64_t plain_n;
   uint8_t nonce[24];
-  int opens;
 } kase;
+typedef struct {
+  uint8_t *crypt;
+  int64_t crypt_n, bad_at;
+  uint8_t tee[16], hash[16], batch[16];
+  int opens;
+} result;
 #define MAXCASE 128
+#define MAXTHREADS 16
 static kase cases[MAXCASE];
+static result results[MAXTHREADS][MAXCASE];
+static int ncases;
 
 /* fs.RangeSeeker on a reader over a crypt file: offset/limit are underlying (crypt file) bytes */
 int32_t goRangeSeek(uintptr_t h, int64_t offset, int32_t whence, int64_t limit) {
@@ -113,13 +128,14 @@ int32_t goRangeSeek(uintptr_t h, int64_t offset, int32_t whence, int64_t limit) 
  * fs.RangeSeeker (RangeSeek moves it, cipher.go:997), odd cases a plain ReadCloser (RangeSeek
  * closes it and opens again, cipher.go:1003-1014). */
 int32_t goOpen(uintptr_t h, int64_t off, int64_t lim, rc_reader *out) {
-  if (h < OPENER_BASE || h - OPENER_BASE >= MAXCASE) return RC_USER_BASE + 1;
-  kase *k = &cases[h - OPENER_BASE];
+  if (h < OPENER_BASE || h - OPENER_BASE >= (uintptr_t)MAXCASE * MAXTHREADS) return RC_USER_BASE + 1;
+  const uintptr_t t = (h - OPENER_BASE) / MAXCASE, i = (h - OPENER_BASE) % MAXCASE;
+  result *k = &results[t][i];
   k->opens++;
   if (off < 0 || off > k->crypt_n) return RC_USER_BASE + 2;
   int64_t end = k->crypt_n;
   if (lim >= 0 && off + lim < end) end = off + lim;
-  *out = gpucipher_reader(new_box(k->crypt, off, end, k->crypt_n, 7000), 1, (h - OPENER_BASE) % 2 == 0);
+  *out = gpucipher_reader(new_box(k->crypt, off, end, k->crypt_n, 7000), 1, i % 2 == 0);
   return RC_NIL;
 }
 
@@ -184,36 +200,20 @@ static int64_t drain(read_fn rd, void *h, uint8_t *dst, int64_t cap, int32_t *er
   }
 }
 
-int main(int argc, char **argv) {
-  if (argc != 2) {
-    fprintf(stderr, "usage: c_client_gpu <manifest>\n");
-    return 2;
-  }
-  FILE *mf = fopen(argv[1], "r");
-  if (!mf) return 2;
-  char keyhex[80], nhex[80], ppath[4096], opath[4096];
-  uint8_t key[32], zero[32] = {0};
-  if (fscanf(mf, "%79s", keyhex) != 1 || unhex(keyhex, key, 32)) return 2;
-  int n = 0;
-  static char outs[MAXCASE][4096];
-  while (n < MAXCASE && fscanf(mf, "%79s %4095s %4095s", nhex, ppath, opath) == 3) {
-    kase *k = &cases[n];
-    if (unhex(nhex, k->nonce, 24)) return 2;
-    k->plain = slurp(ppath, &k->plain_n);
-    if (!k->plain) return 2;
-    memcpy(outs[n], opath, sizeof opath);
-    n++;
-  }
-  fclose(mf);
+/* every check of every case, on one thread, into results[t] */
+typedef struct {
+  rc_cipher *c;
+  int t;
+} job;
 
-  /* Cipher with keys from the Go side's Cipher.Key (New(dataKey, nameKey, nameTweak, ..)) */
+static void *run_cases(void *arg) {
+  rc_cipher *c = ((job *)arg)->c;
+  const int t = ((job *)arg)->t;
+  const int n = ncases;
   int32_t err = RC_NIL;
-  rc_cipher *c = rc_cipher_new(NULL, NULL, &err);
-  if (!c) return 2;
-  rc_cipher_set_keys(c, key, zero, zero);
-
   for (int i = 0; i < n; i++) {
-    kase *k = &cases[i];
+    const kase *k = &cases[i];
+    result *res = &results[t][i];
     const int64_t want_n = rc_encrypted_size(k->plain_n);
     const int64_t nblocks = (k->plain_n + 65535) / 65536;
 
@@ -226,22 +226,16 @@ int main(int argc, char **argv) {
     uint8_t en[24]; /* the nonce the object is stored under, visible before the first Read (crypt.go:529) */
     rc_encrypter_nonce(e, en);
     CHECK(!memcmp(en, k->nonce, 24), "case %d: encrypter nonce", i);
-    k->crypt = (uint8_t *)malloc((size_t)want_n + 1);
-    k->crypt_n = drain(enc_read, e, k->crypt, want_n + 1, &err);
-    CHECK(err == RC_EOF && k->crypt_n == want_n, "case %d: encrypt read %lld of %lld, err %d", i,
-          (long long)k->crypt_n, (long long)want_n, err);
-    uint8_t tee[16];
-    CHECK(rc_encrypter_md5(e, tee) == RC_NIL, "case %d: tee md5", i);
+    res->crypt = (uint8_t *)malloc((size_t)want_n + 1);
+    res->crypt_n = drain(enc_read, e, res->crypt, want_n + 1, &err);
+    CHECK(err == RC_EOF && res->crypt_n == want_n, "case %d: encrypt read %lld of %lld, err %d", i,
+          (long long)res->crypt_n, (long long)want_n, err);
+    CHECK(rc_encrypter_md5(e, res->tee) == RC_NIL, "case %d: tee md5", i);
     rc_encrypter_free(e);
-    FILE *of = fopen(outs[i], "wb");
-    if (of) {
-      fwrite(k->crypt, 1, (size_t)k->crypt_n, of);
-      fclose(of);
-    }
 
     /* ---- decrypt (DecryptData over an io.ReadCloser that is also a RangeSeeker) */
     uint8_t *back = (uint8_t *)malloc((size_t)k->plain_n + 1);
-    uintptr_t rc = new_box(k->crypt, 0, k->crypt_n, k->crypt_n, 7000);
+    uintptr_t rc = new_box(res->crypt, 0, res->crypt_n, res->crypt_n, 7000);
     rc_decrypter *d = gpucipher_decrypt(c, rc, 1, &err);
     CHECK(d && err == RC_NIL, "case %d: gpucipher_decrypt %d", i, err);
     if (d) {
@@ -258,7 +252,7 @@ int main(int argc, char **argv) {
     int64_t off = k->plain_n > 70050 ? 70000 : k->plain_n / 2;
     int64_t lim = 50;
     int32_t wrapped = -1;
-    d = gpucipher_decrypt_seek(c, OPENER_BASE + (uintptr_t)i, off, lim, &err, &wrapped);
+    d = gpucipher_decrypt_seek(c, OPENER_BASE + (uintptr_t)(MAXCASE * t + i), off, lim, &err, &wrapped);
     CHECK(d && err == RC_NIL, "case %d: gpucipher_decrypt_seek %d (wrapped %d)", i, err, wrapped);
     if (d) {
       int64_t expect = k->plain_n - off < lim ? k->plain_n - off : lim;
@@ -279,28 +273,29 @@ int main(int argc, char **argv) {
     /* ---- tampered ciphertext: one byte of block nblocks/2's payload flipped.  The decrypter
      * returns every byte before that block, then ErrorEncryptedBadBlock (cipher.go:880-893),
      * which the Go side maps to the sentinel Register() installed for RC_ERR_BAD_BLOCK. */
-    int64_t bad_at = -1;
+    res->bad_at = -1;
     if (nblocks > 0) {
       const int64_t kb = nblocks / 2;
-      uint8_t *t = (uint8_t *)malloc((size_t)k->crypt_n);
-      memcpy(t, k->crypt, (size_t)k->crypt_n);
-      t[32 + kb * 65552 + 16] ^= 0x40;
-      uintptr_t tr = new_box(t, 0, k->crypt_n, k->crypt_n, 0);
+      uint8_t *tb = (uint8_t *)malloc((size_t)res->crypt_n);
+      memcpy(tb, res->crypt, (size_t)res->crypt_n);
+      tb[32 + kb * 65552 + 16] ^= 0x40;
+      uintptr_t tr = new_box(tb, 0, res->crypt_n, res->crypt_n, 0);
       d = gpucipher_decrypt(c, tr, 0, &err);
       CHECK(d && err == RC_NIL, "case %d: decrypt tampered %d", i, err);
       if (d) {
-        bad_at = drain(dec_read, d, back, k->plain_n + 1, &err);
-        CHECK(err == RC_ERR_BAD_BLOCK && bad_at == kb * 65536 && !memcmp(back, k->plain, (size_t)bad_at),
-              "case %d: tampered block %lld -> err %d after %lld bytes", i, (long long)kb, err, (long long)bad_at);
+        res->bad_at = drain(dec_read, d, back, k->plain_n + 1, &err);
+        CHECK(err == RC_ERR_BAD_BLOCK && res->bad_at == kb * 65536 && !memcmp(back, k->plain, (size_t)res->bad_at),
+              "case %d: tampered block %lld -> err %d after %lld bytes", i, (long long)kb, err,
+              (long long)res->bad_at);
         CHECK(!strcmp(rc_error_string(err), "failed to authenticate decrypted block - bad password?"),
               "case %d: bad-block message", i);
         rc_decrypter_close(d);
         rc_decrypter_free(d);
       }
       /* a tampered tag (the block's first 16 bytes) fails the same way */
-      memcpy(t, k->crypt, (size_t)k->crypt_n);
-      t[32 + kb * 65552] ^= 0x01;
-      tr = new_box(t, 0, k->crypt_n, k->crypt_n, 0);
+      memcpy(tb, res->crypt, (size_t)res->crypt_n);
+      tb[32 + kb * 65552] ^= 0x01;
+      tr = new_box(tb, 0, res->crypt_n, res->crypt_n, 0);
       d = gpucipher_decrypt(c, tr, 0, &err);
       if (d) {
         int64_t got = drain(dec_read, d, back, k->plain_n + 1, &err);
@@ -308,22 +303,15 @@ int main(int argc, char **argv) {
         rc_decrypter_close(d);
         rc_decrypter_free(d);
       }
-      free(t);
+      free(tb);
     }
     free(back);
 
     /* ---- computeHashWithNonce, one object (the cryptcheck checker's call) */
-    uint8_t hash[16];
     uintptr_t src = new_box(k->plain, 0, k->plain_n, k->plain_n, 3000);
-    CHECK(gpucipher_compute_hash(c, src, 1, k->nonce, hash) == RC_NIL && boxes[src].closes == 1,
+    CHECK(gpucipher_compute_hash(c, src, 1, k->nonce, res->hash) == RC_NIL && boxes[src].closes == 1,
           "case %d: compute hash", i);
-    CHECK(!memcmp(hash, tee, 16), "case %d: computeHashWithNonce == put's tee MD5", i);
-
-    char th[33], hh[33];
-    hexs(th, tee, 16);
-    hexs(hh, hash, 16);
-    printf("case %d size %lld tee %s hash %s bad_block_at %lld opens %d\n", i, (long long)k->plain_n, th, hh,
-           (long long)bad_at, k->opens);
+    CHECK(!memcmp(res->hash, res->tee, 16), "case %d: computeHashWithNonce == put's tee MD5", i);
   }
 
   /* ---- computeHashWithNonce batched over every case (HashBatchWithNonce) */
@@ -337,14 +325,89 @@ int main(int argc, char **argv) {
   }
   CHECK(gpucipher_hash_batch(c, (uint64_t)n, srcs, (uint64_t)n, nonces, md5, errs) == RC_NIL, "hash batch");
   for (int i = 0; i < n; i++) {
-    char bh[33];
-    hexs(bh, md5 + 16 * i, 16);
     CHECK(errs[i] == RC_NIL && boxes[srcs[i]].closes == 1, "batch %d: err %d", i, errs[i]);
+    memcpy(results[t][i].batch, md5 + 16 * i, 16);
+  }
+  free(srcs);
+  free(nonces);
+  free(md5);
+  free(errs);
+  return NULL;
+}
+
+int main(int argc, char **argv) {
+  if (argc != 2 && argc != 3) {
+    fprintf(stderr, "usage: c_client_gpu <manifest> [threads]\n");
+    return 2;
+  }
+  const int nthreads = argc == 3 ? atoi(argv[2]) : 1;
+  if (nthreads < 1 || nthreads > MAXTHREADS) return 2;
+  FILE *mf = fopen(argv[1], "r");
+  if (!mf) return 2;
+  char keyhex[80], nhex[80], ppath[4096], opath[4096];
+  uint8_t key[32], zero[32] = {0};
+  if (fscanf(mf, "%79s", keyhex) != 1 || unhex(keyhex, key, 32)) return 2;
+  int n = 0;
+  static char outs[MAXCASE][4096];
+  while (n < MAXCASE && fscanf(mf, "%79s %4095s %4095s", nhex, ppath, opath) == 3) {
+    kase *k = &cases[n];
+    if (unhex(nhex, k->nonce, 24)) return 2;
+    k->plain = slurp(ppath, &k->plain_n);
+    if (!k->plain) return 2;
+    memcpy(outs[n], opath, sizeof opath);
+    n++;
+  }
+  fclose(mf);
+  ncases = n;
+
+  /* one Cipher with keys from the Go side's Cipher.Key (New(dataKey, nameKey, nameTweak, ..)),
+   * shared by every thread as rclone shares it between its goroutines */
+  int32_t err = RC_NIL;
+  rc_cipher *c = rc_cipher_new(NULL, NULL, &err);
+  if (!c) return 2;
+  rc_cipher_set_keys(c, key, zero, zero);
+
+  job jobs[MAXTHREADS];
+  pthread_t th[MAXTHREADS];
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t] = (job){c, t};
+    if (nthreads == 1) run_cases(&jobs[t]);
+    else if (pthread_create(&th[t], NULL, run_cases, &jobs[t]) != 0) return 2;
+  }
+  if (nthreads > 1)
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+
+  /* every thread produced thread 0's bytes and digests */
+  for (int t = 1; t < nthreads; t++)
+    for (int i = 0; i < n; i++) {
+      const result *a = &results[0][i], *b = &results[t][i];
+      CHECK(a->crypt && b->crypt && a->crypt_n == b->crypt_n && !memcmp(a->crypt, b->crypt, (size_t)a->crypt_n) &&
+                !memcmp(a->tee, b->tee, 16) && !memcmp(a->hash, b->hash, 16) && !memcmp(a->batch, b->batch, 16) &&
+                a->bad_at == b->bad_at && a->opens == b->opens,
+            "thread %d case %d differs from thread 0", t, i);
+    }
+  for (int i = 0; i < n; i++) {
+    const result *r = &results[0][i];
+    FILE *of = fopen(outs[i], "wb");
+    if (of) {
+      if (r->crypt) fwrite(r->crypt, 1, (size_t)r->crypt_n, of);
+      fclose(of);
+    }
+    char th_[33], hh[33];
+    hexs(th_, r->tee, 16);
+    hexs(hh, r->hash, 16);
+    printf("case %d size %lld tee %s hash %s bad_block_at %lld opens %d\n", i, (long long)cases[i].plain_n, th_, hh,
+           (long long)r->bad_at, r->opens);
+  }
+  for (int i = 0; i < n; i++) {
+    char bh[33];
+    hexs(bh, results[0][i].batch, 16);
     printf("batch %d %s\n", i, bh);
   }
+  if (nthreads > 1) printf("threads %d consistent\n", nthreads);
   rc_cipher_free(c);
-  if (failures) {
-    fprintf(stderr, "%d failures\n", failures);
+  if (atomic_load(&failures)) {
+    fprintf(stderr, "%d failures\n", atomic_load(&failures));
     return 1;
   }
   printf("c client gpu ok\n");

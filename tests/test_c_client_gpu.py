@@ -15,8 +15,11 @@ ones with the 192-bit nonce carry included.  Checks:
   50), a RangeSeek on the same handle, and a tampered payload byte / tag -> every byte before the
   bad block, then ErrorEncryptedBadBlock, at exactly that block.
 
-`-m gpu`: the real library on the device.  CPU suite: the same client over the host C++ with the
-GPU replaced by the CPU oracle (tests/native/stub_engine.cpp, test-only), under ASan + UBSan.
+`-m gpu`: the real library on the device, once on one thread and once with 4 threads running
+every case at once over the one shared cipher (the Go side's --transfers goroutines calling
+through the shim concurrently; every thread's bytes and digests must equal thread 0's).  CPU
+suite: the same client over the host C++ with the GPU replaced by the CPU oracle
+(tests/native/stub_engine.cpp, test-only), under ASan + UBSan, with 3 threads.
 """
 import hashlib
 import os
@@ -53,7 +56,7 @@ def _cases(ref_kat, sodium_vectors, sodium_pick):
     return [(bytes(32), ref), (bytes.fromhex(sodium_vectors["key"]), sod)]
 
 
-def _run_group(exe, tmp_path, tag, key, cases, timeout):
+def _run_group(exe, tmp_path, tag, key, cases, timeout, threads=1):
     manifest = tmp_path / f"{tag}.manifest"
     lines = [key.hex()]
     for i, (nonce, plain, *_rest) in enumerate(cases):
@@ -63,9 +66,11 @@ def _run_group(exe, tmp_path, tag, key, cases, timeout):
     manifest.write_text("\n".join(lines) + "\n")
     env = dict(os.environ)
     env.setdefault("ASAN_OPTIONS", "detect_leaks=0")
-    r = subprocess.run([exe, str(manifest)], capture_output=True, text=True, timeout=timeout, env=env)
+    r = subprocess.run([exe, str(manifest), str(threads)], capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert r.stdout.rstrip().endswith("c client gpu ok")
+    if threads > 1:
+        assert f"threads {threads} consistent" in r.stdout
     rows = {}
     batch = {}
     for line in r.stdout.splitlines():
@@ -111,7 +116,7 @@ def test_shim_data_path_cpu_stub(stub_client, tmp_path, ref_kat, sodium_vectors)
     pick = lambda files: [i for i, f in enumerate(files)  # noqa: E731
                           if f["plain"] == "splitmix64" and (f["size"] > 131072 or f["size"] in (0, 17, 65536))]
     for tag, (key, cases) in zip(("ref", "sod"), _cases(ref_kat, sodium_vectors, pick)):
-        _run_group(stub_client, tmp_path, tag, key, cases, timeout=300)
+        _run_group(stub_client, tmp_path, tag, key, cases, timeout=300, threads=3)
 
 
 @pytest.mark.gpu
@@ -124,6 +129,7 @@ def test_shim_data_path_gpu(tmp_path, ref_kat, sodium_vectors):
     _lib.lib()  # librclone_crypt.so current (the build id the suite reports)
     subprocess.check_call(["make", "-s", "-C", NATIVE, "build/c_client_gpu"])
     exe = os.path.join(NATIVE, "build", "c_client_gpu")
-    for tag, (key, cases) in zip(("ref", "sod"), _cases(ref_kat, sodium_vectors, _all_multiblock_and_edges)):
-        rows = _run_group(exe, tmp_path, tag, key, cases, timeout=120)
-        print(tag, len(rows), "cases through the shim on the GPU")
+    for threads in (1, 4):
+        for tag, (key, cases) in zip(("ref", "sod"), _cases(ref_kat, sodium_vectors, _all_multiblock_and_edges)):
+            rows = _run_group(exe, tmp_path, f"{tag}{threads}", key, cases, timeout=120, threads=threads)
+            print(tag, len(rows), "cases through the shim on the GPU,", threads, "thread(s)")
