@@ -232,6 +232,31 @@ def test_splitmix_block_stream():
         assert splitmix64_block(7, g) == whole[g * 65536:(g + 1) * 65536]
 
 
+def test_random_source():
+    # TestRandomSource (cipher_test.go:1054-1067): the test infrastructure first.  The reference
+    # copies 1e8 bytes; 1e6 here (every byte crosses Python).  The vectorised form the parity
+    # tests use (testdata.random_source) is the same sequence.
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from go_readers import EOF, RandomSource
+
+    from rclone_amd.testdata import random_source
+    n = 10**6
+    source, sink = RandomSource(n), RandomSource(n)
+    copied = 0
+    while True:
+        p, err = source.read_go(32768)
+        copied += sink.write(p)
+        if err is EOF:
+            break
+    assert copied == n
+    assert RandomSource(70000).read_go(70001) == (random_source(70000), EOF)
+    source = RandomSource(n)
+    source.read_go(16)
+    with pytest.raises(AssertionError, match="Error in stream at 1$"):
+        RandomSource(n).write(source.read_go(32768)[0])
+
+
 def test_device_entry_points_reject_bad_arguments():
     # argument checks run before any HIP call, so they hold on a machine without a GPU
     import ctypes
