@@ -67,6 +67,9 @@ ErrorFileClosed = _sentinel("ErrorFileClosed", "file already closed")
 ErrorBadSeek = _sentinel("ErrorBadSeek", "Seek beyond end of file")
 ErrUnexpectedEOF = _sentinel("ErrUnexpectedEOF", "unexpected EOF")
 GPUError = _sentinel("GPUError", "GPU crypt engine failure")
+# io.EOF where the reference returns it as a call's only error (RangeSeek at the end of a
+# whole-block file, DecryptDataSeek opened there: cipher.go:1019-1022, :848-853), not a Read's
+ErrEOF = _sentinel("ErrEOF", "EOF")
 
 _CODE_TO_CLASS = {
     -101: ErrorEncryptedFileTooShort,
@@ -76,6 +79,7 @@ _CODE_TO_CLASS = {
     -105: ErrorFileClosed,
     -106: ErrorBadSeek,
     -120: GPUError,
+    RC_EOF: ErrEOF,
     RC_UNEXPECTED_EOF: ErrUnexpectedEOF,
 }
 
@@ -514,8 +518,8 @@ class Decrypter:
             w = ctypes.c_int32(0)
             self._h = _lib.lib().rc_decrypt_data_seek_ex(cipher._h, self._open_cb, None, offset, limit, ctypes.byref(e),
                                                          ctypes.byref(w))
-            if not self._h:
-                _raise(e.value, wrapped=w.value)  # RC_ERR_REOPEN: the opener's own error as the cause
+            if not self._h and e.value != RC_NIL:  # RC_ERR_REOPEN: the opener's own error as the cause
+                raise _ERRS.exc(e.value, w.value)  # (RC_EOF too: newDecrypterSeek's RangeSeek hit the end)
         if not self._h:
             _raise(e.value)
             raise GPUError(GPUError.message)

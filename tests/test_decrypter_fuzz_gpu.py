@@ -1,0 +1,123 @@
+"""Randomised operation sequences on the GPU decrypter against the reference's state machine.
+
+Each case encrypts a random-size object with the CPU oracle (sometimes with one block tampered),
+opens it through DecryptDataSeek at a random (offset, limit) -- beyond the end included -- and runs
+a random sequence of Read (1 byte .. 100 KB), RangeSeek (random offset and limit) and Seek calls
+(io.SeekStart, and now and then io.SeekCurrent, which the reference refuses and makes sticky).
+The GPU decrypter (librclone_crypt.so through the rc_* C ABI: read-ahead batches, the engine's
+ranged opens that decrypt only the 4 KiB groups a limit reaches, pass_bad_blocks) must return,
+call by call, the same bytes and the same error as tests/go_decrypter_model.py, the step-by-step
+restatement of backend/crypt/cipher.go:776-1087 that tests/test_decrypter_model.py pins to the
+reference's own decrypter tests.  Construction errors (the header, a seek past the end) must
+match too, and Close must close once.
+"""
+import random
+
+import pytest
+
+from oracle import pyoracle as orc
+from rclone_amd import crypt
+from rclone_amd.crypt import EOF
+from tests.go_decrypter_model import ModelDecrypter, kind
+from tests.go_readers import Buffer
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+BLOCK_DATA = 65536
+BLOCK_SIZE = 65552
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _opener(ct):
+    def open_fn(off, lim):
+        end = len(ct) if lim < 0 else min(off + lim, len(ct))
+        return Buffer(ct[off:end])
+    return open_fn
+
+
+def _size(rng):
+    return rng.choice([0, 1, 17, 4096, 65535, 65536, 65537, 131072, 131073, 200000, 5 * 65536 + 4321,
+                       rng.randrange(1, 6 * 65536)])
+
+
+def _offset_limit(rng, size):
+    off = rng.choice([0, 0, size, max(size - 1, 0), rng.randrange(0, size + 2), rng.randrange(0, size + 70000),
+                      (rng.randrange(0, 7) * BLOCK_DATA)])
+    lim = rng.choice([-1, -1, 0, 1, 4096, rng.randrange(0, 200000), max(size - off, 0)])
+    return off, lim
+
+
+def _construct(cls, *a, **kw):
+    try:
+        return cls(*a, **kw), None
+    except crypt.CryptError as e:
+        return None, e
+
+
+@pytest.mark.parametrize("batch", [1, 3, 64])
+def test_decrypter_sequences_match_reference(batch):
+    rng = random.Random(0xDEC0 + batch)
+    cases = ops_run = 0
+    for case in range(70):
+        size = _size(rng)
+        plain = bytes(rng.getrandbits(8) for _ in range(min(size, 64))) * (size // 64 + 1)
+        plain = plain[:size]
+        nonce = bytes(rng.getrandbits(8) for _ in range(24))
+        if case % 5 == 0:
+            nonce = b"\xff" * 8 + nonce[8:]  # block nonces carry past byte 8
+        ct = bytearray(orc.encrypt_file(plain, nonce, bytes(32)))
+        nblk = (size + BLOCK_DATA - 1) // BLOCK_DATA
+        if nblk and rng.random() < 0.3:  # one tampered block: tag or payload byte
+            b = rng.randrange(nblk)
+            blen = min(BLOCK_SIZE, len(ct) - 32 - b * BLOCK_SIZE)
+            ct[32 + b * BLOCK_SIZE + rng.randrange(blen)] ^= 1 << rng.randrange(8)
+        ct = bytes(ct)
+        pbb = rng.random() < 0.25
+        c = crypt.Cipher("", "", batch_blocks=batch, pass_bad_blocks=pbb)
+        off, lim = _offset_limit(rng, size)
+        model, merr = _construct(ModelDecrypter, bytes(32), _opener(ct), off, lim, pass_bad_blocks=pbb)
+        try:
+            gpu, gerr = c.decrypt_data_seek(_opener(ct), off, lim), None
+        except crypt.CryptError as e:
+            gpu, gerr = None, e
+        where = f"case {case} size {size} open ({off}, {lim}) pbb {pbb}"
+        assert kind(gerr) == kind(merr), (where, gerr, merr)
+        cases += 1
+        if model is None:
+            continue
+        for step in range(14):
+            r = rng.random()
+            if r < 0.6:
+                n = rng.choice([1, 7, 4096, 65536, 65537, 100000, rng.randrange(1, 140000)])
+                got, gerr = gpu.read_go(n)
+                want, merr = model.read_go(n)
+                assert (got == want, kind(gerr)) == (True, kind(merr)), (where, step, "read", n, len(got), len(want),
+                                                                         gerr, merr)
+            elif r < 0.95:
+                o, l2 = _offset_limit(rng, size)
+                try:
+                    gres, gerr = gpu.range_seek(o, 0, l2), None
+                except crypt.CryptError as e:
+                    gres, gerr = 0, e
+                mres, merr = model.range_seek(o, 0, l2)
+                assert (gres, kind(gerr)) == (mres, kind(merr)), (where, step, "range_seek", o, l2, gerr, merr)
+            else:
+                o = rng.randrange(0, size + 2)
+                try:
+                    gres, gerr = gpu.seek(o, 1), None
+                except crypt.CryptError as e:
+                    gres, gerr = 0, e
+                mres, merr = model.range_seek(o, 1, -1)
+                assert (gres, kind(gerr)) == (mres, kind(merr)), (where, step, "seek whence 1", gerr, merr)
+            ops_run += 1
+        gpu.close()
+        assert model.close() is None
+        with pytest.raises(crypt.ErrorFileClosed):
+            gpu.close()
+    print(f"batch {batch}: {cases} handles, {ops_run} calls matched the reference's state machine")
