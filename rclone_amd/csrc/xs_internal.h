@@ -67,9 +67,20 @@ constexpr int XS_INLINE_DESCS = 16;
 // kernels act on it (full blocks); every other path writes all bytes.
 constexpr uint32_t XS_DESC_WINDOW = 0x80000000u;
 constexpr uint64_t XS_WINDOW_GROUP = 4096;
+// A fused batch of at most XS_KEY_PRE blocks (a ranged read: one or two) also carries each block's
+// key setup, derived on the host while the launch is prepared: the HSalsa20 subkey and words 0..7
+// of keystream blocks 0 (Poly1305 r, s) and 1024 (the last two chunks).  Three Salsa20 cores per
+// block (~0.3 us on one host core) that would otherwise sit in front of the kernel's power tables
+// and keystream, one after the other.
+constexpr int XS_KEY_PRE = 2;
+struct XsKeyPre {
+  uint32_t sk[8], k0[8], k1024[8];
+};
 struct XsInlineDescs {
   xs_block_desc d[XS_INLINE_DESCS];
-  uint32_t n;  // d[0..n) valid; blocks >= n read desc
+  XsKeyPre pre[XS_KEY_PRE];
+  uint32_t n;     // d[0..n) valid; blocks >= n read desc
+  uint32_t npre;  // pre[0..npre) valid (blocks >= npre derive their key setup in the kernel)
 };
 hipError_t launch_crypt_fused(bool seal, const KeyArg& key, const NonceArg& bounds, const xs_block_desc* desc,
                               const xs_block_desc* host_desc, uint64_t nblocks, const uint8_t* src, uint8_t* dst,

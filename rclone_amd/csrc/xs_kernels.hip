@@ -30,6 +30,9 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
 
 #include "xs_internal.h"
 #include "xs_salsa_lazy.h"
@@ -721,7 +724,8 @@ template <int MODE, class Mid = KgNoMid>
 __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32_t n[6], uint64_t src, uint64_t dst,
                                                  uint32_t len, BlockKey* o, const uint32_t* sk_lds,
                                                  const uint32_t* sk_flag, const Mid& mid = Mid(),
-                                                 uint32_t* cd_flag = nullptr);
+                                                 uint32_t* cd_flag = nullptr, bool use_kp = false,
+                                                 const XsKeyPre& kp = XsKeyPre{});
 
 // sk_lds / sk_flag (LDS, optional): take the HSalsa20 subkey another wave of the workgroup derives
 // for the same block (its LDS writes completed, then *sk_flag raised) instead of computing it
@@ -747,14 +751,19 @@ __device__ __forceinline__ void keygen_wave(const KeyArg& key, const NonceArg& n
 
 // The key schedule of one block whose descriptor fields are already known (and valid).  For a
 // full block, mid() runs once the A and B power tables are in *o (before C, D and the correction
-// term): the fused kernel builds its Toeplitz table there and lets the crypt waves go on.
+// term): the fused kernel builds its Toeplitz table there and lets the crypt waves go on.  With
+// use_kp, kp is the block's key setup derived on the host (XsKeyPre): no Salsa20 core here then.
 template <int MODE, class Mid>
 __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32_t n[6], uint64_t src, uint64_t dst,
                                                  uint32_t len, BlockKey* o, const uint32_t* sk_lds,
-                                                 const uint32_t* sk_flag, const Mid& mid, uint32_t* cd_flag) {
+                                                 const uint32_t* sk_flag, const Mid& mid, uint32_t* cd_flag,
+                                                 bool use_kp, const XsKeyPre& kp) {
   const uint32_t l = threadIdx.x & 63u;
   uint32_t sk[8];
-  if (sk_lds) {
+  if (use_kp) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) sk[i] = kp.sk[i];
+  } else if (sk_lds) {
     lds_wait_subkey(sk_flag, sk_lds, sk);
   } else {
     uint32_t x[16] = {SIG0, key.k[0], key.k[1], key.k[2], key.k[3], SIG1, n[0], n[1],
@@ -766,7 +775,17 @@ __device__ __forceinline__ void keygen_wave_body(const KeyArg& key, const uint32
     sk[4] = x[6]; sk[5] = x[7]; sk[6] = x[8]; sk[7] = x[9];
   }
   uint32_t ks[16];
-  salsa20_block_lazy(sk, n[4], n[5], l < 32 ? 0u : 1024u, ks);
+  if (use_kp) {  // words 0..7 of keystream blocks 0 (lanes < 32) and 1024 (lanes >= 32), as below
+    // Both words are read as wave-uniform (scalar) loads and selected per lane afterwards: a per-lane
+    // choice of address would make them vector loads of the kernel arguments (microseconds)
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint32_t a = __builtin_amdgcn_readfirstlane(kp.k0[i]), b = __builtin_amdgcn_readfirstlane(kp.k1024[i]);
+      ks[i] = as_varying(l < 32 ? a : b);
+    }
+  } else {
+    salsa20_block_lazy(sk, n[4], n[5], l < 32 ? 0u : 1024u, ks);
+  }
   if (l == 32 && len > XS_BLOCK_DATA - 32) {
 #pragma unroll
     for (int i = 0; i < 8; i++) o->ks1024[i] = ks[i];
@@ -1583,6 +1602,66 @@ __device__ __forceinline__ void wave_sum5(P5& h) {
   }
 }
 
+// The key wave of a ranged read's open (a group window: the VALU tag below).  Keystream words
+// 0..7 of blocks 0 (lanes < 32: r, s) and 1024 (lanes >= 32: the last two chunks) -- from the
+// host's key setup, or made here from wave 0's subkey -- go into *kl and raise r_flag.  Then the
+// weight table the crypt waves' Horner sums need, one entry per lane: lane i < 32 holds
+// r^(126 - 4i), lane 32 + j holds r^(128 j), from one square-and-multiply pass over r^(2^s),
+// s = 0..11 (lanes < 32 take bits 1..6, lanes >= 32 bits 7..11), into tab, then tab_flag.
+__device__ __forceinline__ void fused_key_wave_vtag(const uint32_t n[6], BlockKey* kl, const uint32_t* sk_lds,
+                                                    const uint32_t* sk_flag, uint32_t* r_flag, uint32_t (*tab)[5],
+                                                    uint32_t* tab_flag, bool use_kp, const XsKeyPre& kp) {
+  const uint32_t l = threadIdx.x & 63u;
+  uint32_t ks[16];
+  if (use_kp) {  // wave-uniform (scalar) loads, selected per lane afterwards (see keygen_wave_body)
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint32_t a = __builtin_amdgcn_readfirstlane(kp.k0[i]), b = __builtin_amdgcn_readfirstlane(kp.k1024[i]);
+      ks[i] = as_varying(l < 32 ? a : b);
+    }
+  } else {
+    uint32_t sk[8];
+    lds_wait_subkey(sk_flag, sk_lds, sk);
+    salsa20_block_lazy(sk, n[4], n[5], l < 32 ? 0u : 1024u, ks);
+  }
+  if (l == 32) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) kl->ks1024[i] = ks[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) ks[i] = __shfl(ks[i], 0);  // block 0 words 0..7 (r, s) everywhere
+  P5 r;
+  r.v[0] = ks[0] & 0x3ffffffu;
+  r.v[1] = alignbit(ks[1], ks[0], 26) & 0x3ffff03u;
+  r.v[2] = alignbit(ks[2], ks[1], 20) & 0x3ffc0ffu;
+  r.v[3] = alignbit(ks[3], ks[2], 14) & 0x3f03fffu;
+  r.v[4] = (ks[3] >> 8) & 0x00fffffu;
+  if (l == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) kl->s[i] = ks[4 + i];
+#pragma unroll
+    for (int i = 0; i < 5; i++) kl->r[i] = r.v[i];
+  }
+  lds_raise_flag(r_flag);
+  // exponent of this lane's entry: 126 - 4i = 2 + 4 (31 - i) (bit 1 set, bit 0 clear), or 128 j
+  const uint32_t e = l < 32u ? 126u - 4u * l : (l - 32u) << 7;
+  P5 sq = r, acc;
+  acc.v[0] = 1; acc.v[1] = acc.v[2] = acc.v[3] = acc.v[4] = 0;
+#pragma unroll
+  for (int s = 0; s < 12; s++) {
+    const bool take = (e >> s) & 1u;
+    if (s == 1 || s == 7) {  // a lane's first factor (its entry is still 1 there): no multiply
+      if (take) acc = sq;
+    } else if (s > 1) {
+      const P5 q = pmul(acc, sq);
+      if (take) acc = q;
+    }
+    if (s < 11) sq = pmul(sq, sq);
+  }
+  put5(tab[l], acc);
+  lds_raise_flag(tab_flag);
+}
+
 template <bool SEAL, int NCW>
 __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, NonceArg bounds, const xs_block_desc* __restrict__ desc,
                                                                     const XsInlineDescs inl,
@@ -1594,9 +1673,11 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
   static_assert(f2_lds_words<NCW>() >= LDS_WORDS, "the fallback path runs crypt_wave in this LDS");
   __shared__ __attribute__((aligned(16))) uint32_t lds[f2_lds_words<NCW>()];
   __shared__ BlockKey kl;
-  // hs_flag[0..3]: subkeys of waves 0..3 published (for waves 4..7 / the key wave); [4]: Z table ready;
-  // [5]: C and D power tables in kl (wave 0's finalisation factor)
+  // hs_flag[0..3]: subkeys of waves 0..3 published (for waves 4..7 / the key wave); [4]: Z table ready
+  // (a windowed open: r, s and ks1024 in kl); [5]: C and D power tables in kl, wave 0's finalisation
+  // factor (a windowed open: the weight table in vtab).  vpart: each crypt wave's VALU tag sum.
   __shared__ uint32_t hs_key[4][8], hs_flag[6];
+  __shared__ uint32_t vtab[64][5], vpart[NCW][5];
   if (blockIdx.x >= nblocks) return;  // uniform per workgroup (grid == nblocks)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63u;
   const uint64_t blk = blockIdx.x;
@@ -1626,6 +1707,14 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
     if (rsv & XS_DESC_WINDOW) gwin = rsv & 0xFFFFu;
   }
   gwin = __builtin_amdgcn_readfirstlane(gwin);
+  // the smallest batches bring each block's key setup from the host (XsKeyPre): no HSalsa20 in the
+  // crypt waves, no Salsa20 core in front of the key wave's power tables
+  const bool host_key = blk < inl.npre;
+  // A ranged read's open (a group window) computes its tag on the VALU: with only a group or two to
+  // decrypt, the crypt waves are idle once r exists, and a short key chain (11 squarings) replaces
+  // the power tables, the Toeplitz table and the correction term of the matrix-core tag, which stays
+  // the path of whole blocks (there the keystream keeps the VALU busy).  DESIGN.md section 3e.
+  const bool vtag = !SEAL && gwin != 0xFFFFu;
   __syncthreads();  // hs_flag cleared before any wave can poll or raise it
   if (!valid || len != XS_BLOCK_DATA) {
     // rejected descriptor or partial block: the fused-v1 order (the other waves idle)
@@ -1678,7 +1767,10 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
         tail[1] = *reinterpret_cast<const uint4*>(tp + 16);
       }
       uint32_t sk[8];
-      if (NCW == 8 && wave >= 4u) {  // the subkey of wave - 4, which shares this SIMD
+      if (host_key) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) sk[i] = inl.pre[blk].sk[i];
+      } else if (NCW == 8 && wave >= 4u) {  // the subkey of wave - 4, which shares this SIMD
         if (gn != 0u) lds_wait_subkey(&hs_flag[wave - 4u], hs_key[wave - 4u], sk);
       } else {
         uint32_t x[16] = {SIG0, key.k[0], key.k[1], key.k[2], key.k[3], SIG1, nn[0], nn[1],
@@ -1736,6 +1828,10 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
       // more), then C, D and the correction term, which only the finalisation reads (after B2).
       // It shares a SIMD with wave 0 and is the longer chain: it issues first.
       __builtin_amdgcn_s_setprio(3);
+      if (vtag) {
+        fused_key_wave_vtag(nn, &kl, hs_key[0], &hs_flag[0], &hs_flag[4], vtab, &hs_flag[5], host_key,
+                            inl.pre[host_key ? blk : 0]);
+      } else {
       auto z_table = [&]() {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1765,15 +1861,18 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
         row[2] = make_uint4(0u, 0u, 0u, 0u);
         lds_raise_flag(&hs_flag[4]);
       };
-      // the descriptor fields this kernel already holds (no second read over PCIe); wave 0's subkey
-      keygen_wave_body<MODE>(key, nn, soff, doff, len, &kl, hs_key[0], &hs_flag[0], z_table, &hs_flag[5]);
+      // the descriptor fields this kernel already holds (no second read over PCIe); wave 0's subkey,
+      // or the whole key setup from the host
+      keygen_wave_body<MODE>(key, nn, soff, doff, len, &kl, hs_key[0], &hs_flag[0], z_table, &hs_flag[5], host_key,
+                             inl.pre[host_key ? blk : 0]);
+      }
     }
     xs_v4i acc[4][2];
     P5 tl;  // wave 0, lane 63: the Poly1305 terms of chunks 4094, 4095
 #pragma unroll
     for (int i = 0; i < 5; i++) tl.v[i] = 0;
     if (wave < NCW) {
-      lds_wait_flag(&hs_flag[4]);  // the Z table (each wave reads only its own staged groups)
+      lds_wait_flag(&hs_flag[4]);  // the Z table (each wave reads only its own staged groups); vtag: r
       if (wave == 0 && l == 63u) {
         // chunks 4094, 4095 (keystream block 1024 words 0..7): exponents 2 and 1.  r and ks1024
         // are in kl before the Z flag rises, so this leaves the finalisation's critical path.
@@ -1792,6 +1891,65 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
           tl = pmul(tl, rr);
         }
       }
+      if (vtag) {
+        // ---- phase 2, windowed open: Poly1305 of the LDS-resident ciphertext on the VALU.  Lane l
+        // takes, in each of the wave's 4 KiB groups u, the four consecutive chunks at stage slots
+        // 256u + 4l + j (slot = chunk index + 2: slots 0 and 1 are the key slots and hash nothing),
+        // Horner with r: h_u = sum_j c r^(4 - j).  The wave's groups are consecutive (u0..u1), so
+        // H = sum_u h_u r^(256 (u1 - u)) (Horner with r^256), and H r^(254 - 4l) r^(256 (15 - u1))
+        // gives slot 256u + 4l + j the power r^(4098 - slot), i.e. chunk k its r^(4096 - k).  That
+        // weight is two entries of the key wave's table: r^(126 - 4 (l & 31)) and r^(128 jx),
+        // jx = 2 (15 - u1) + [l < 32].  The wave sums its lanes; wave 0 adds the waves after B2.
+        P5 part;
+#pragma unroll
+        for (int i = 0; i < 5; i++) part.v[i] = 0;
+        const uint32_t g0 = f2_first<NCW>(wave), gn = f2_count<NCW>(wave);
+        if (gn != 0u) {
+          P5 rr;
+#pragma unroll
+          for (int i = 0; i < 5; i++) rr.v[i] = kl.r[i];
+          const PMul R = pmul_prep(rr);
+          P5 h[f2_max_groups<NCW>()];
+#pragma unroll
+          for (uint32_t g = 0; g < (uint32_t)f2_max_groups<NCW>(); g++) {
+#pragma unroll
+            for (int i = 0; i < 5; i++) h[g].v[i] = 0;
+            if (g >= gn) continue;
+            const uint32_t u = g0 + g;
+            const uint4* mine = reinterpret_cast<const uint4*>(stage + 1024 * u + 256 * (l >> 4) + 4 * (l & 15u));
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              const uint4 v = mine[16 * j];
+              if (j >= 2 || u > 0u || l > 0u) padd_full(h[g], v.x, v.y, v.z, v.w);
+              h[g] = pmul_u(h[g], R);
+            }
+          }
+          lds_wait_flag(&hs_flag[5]);  // the weight table
+          const uint32_t u1 = g0 + gn - 1u;
+          const uint32_t jx = 2u * (15u - u1) + (l < 32u ? 1u : 0u);
+          P5 t1, t2, r256;
+#pragma unroll
+          for (int i = 0; i < 5; i++) {
+            t1.v[i] = vtab[l & 31u][i];
+            t2.v[i] = vtab[32u + jx][i];
+            r256.v[i] = vtab[34][i];  // r^(128 * 2)
+          }
+          const P5 tw = pmul(t1, t2);
+          P5 H = h[0];
+#pragma unroll
+          for (uint32_t g = 1; g < (uint32_t)f2_max_groups<NCW>(); g++) {
+            if (g >= gn) break;
+            H = pmul(H, r256);
+            add5(H, h[g]);
+            pnorm(H);
+          }
+          part = pmul(H, tw);
+        }
+        add5(part, tl);  // zero except in wave 0, lane 63
+        pnorm(part);
+        wave_sum5(part);
+        if (l == 0u) put5(vpart[wave], part);
+      } else {
       // ---- phase 2: matrix-core Poly1305 over the LDS-resident ciphertext
       const uint32_t zlo = (15u - n) >> 2, zsh = (31u - n) & 3u;
       uint32_t zaddr = (uint32_t)(uintptr_t)((const lds_u32*)zt + 12u * kg + zlo);
@@ -1841,9 +1999,10 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
           for (int mt = 0; mt < 2; mt++)
             *reinterpret_cast<xs_v4i*>(xacc + (wave - 1u) * 2048u + (uint32_t)(2 * j + mt) * 256u + 4u * l) = acc[j][mt];
       }
+      }
     }
     P5 rexp;  // wave 0: its lane's column exponent r^e, e = 66 - (4n + kg), formed before B2
-    if (wave == 0) {
+    if (wave == 0 && !vtag) {
       lds_wait_flag(&hs_flag[5]);  // C and D are in kl
       const uint32_t e = 66u - (4u * n + kg);
       P5 t1, t2;
@@ -1856,6 +2015,19 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
     }
     __syncthreads();  // B2: the other waves' accumulators are in LDS
     if (wave == 0) {
+      const BlockKey* bk = &kl;
+      P5 hs;
+      if (vtag) {  // the waves' sums (each < 2^27 + 2^7)
+#pragma unroll
+        for (int i = 0; i < 5; i++) hs.v[i] = 0;
+        if (l == 0u) {
+#pragma unroll
+          for (int w = 0; w < NCW; w++) {
+#pragma unroll
+            for (int i = 0; i < 5; i++) hs.v[i] += vpart[w][i];
+          }
+        }
+      } else {
 #pragma unroll
       for (int w = 0; w < NCW - 1; w++)
 #pragma unroll
@@ -1885,8 +2057,7 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
           xw[4 + kk] = v.y;
         }
       }
-      const BlockKey* bk = &kl;
-      P5 hs = pmul(column_value(xw), rexp);
+      hs = pmul(column_value(xw), rexp);
       if (l == 0u) {
 #pragma unroll
         for (int i = 0; i < 5; i++) hs.v[i] += bk->corr[i];
@@ -1897,6 +2068,7 @@ __global__ void __launch_bounds__(64 * (NCW + 1)) xs_crypt_fused2(KeyArg key, No
       }
       pnorm(hs);
       wave_sum5(hs);
+      }
       uint32_t verdict = 1;
       if (l == 0) {
         const P5 hc = pcanon(hs);
@@ -2001,14 +2173,56 @@ hipError_t launch_crypt(bool seal, const BlockKey* keys, uint64_t nblocks, const
   return hipGetLastError();
 }
 
+// ---- host key setup for the smallest fused batches (XsKeyPre): the same Salsa20 core as the
+// kernels' (salsa20_block / HSalsa20 of keygen), on one host core
+static inline uint32_t hrotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+static void host_salsa_rounds(uint32_t (&x)[16]) {
+  for (int i = 0; i < 10; i++) {
+#define XS_HQR(a, b, c, d)        \
+  x[b] ^= hrotl(x[a] + x[d], 7);  \
+  x[c] ^= hrotl(x[b] + x[a], 9);  \
+  x[d] ^= hrotl(x[c] + x[b], 13); \
+  x[a] ^= hrotl(x[d] + x[c], 18);
+    XS_HQR(0, 4, 8, 12) XS_HQR(5, 9, 13, 1) XS_HQR(10, 14, 2, 6) XS_HQR(15, 3, 7, 11)
+    XS_HQR(0, 1, 2, 3) XS_HQR(5, 6, 7, 4) XS_HQR(10, 11, 8, 9) XS_HQR(15, 12, 13, 14)
+#undef XS_HQR
+  }
+}
+static void host_key_pre(const KeyArg& key, const uint8_t nonce[24], XsKeyPre& p) {
+  uint32_t n[6];
+  memcpy(n, nonce, 24);  // little-endian words, as the kernels' nonce words
+  uint32_t x[16] = {SIG0, key.k[0], key.k[1], key.k[2], key.k[3], SIG1, n[0], n[1],
+                    n[2], n[3],     SIG2,     key.k[4], key.k[5], key.k[6], key.k[7], SIG3};
+  host_salsa_rounds(x);  // HSalsa20: no feed-forward; words 0, 5, 10, 15, 6..9
+  const uint32_t sk[8] = {x[0], x[5], x[10], x[15], x[6], x[7], x[8], x[9]};
+  memcpy(p.sk, sk, sizeof sk);
+  for (int b = 0; b < 2; b++) {
+    const uint32_t ctr = b ? 1024u : 0u;
+    const uint32_t in[16] = {SIG0, sk[0], sk[1], sk[2], sk[3], SIG1, n[4], n[5], ctr, 0u, SIG2, sk[4], sk[5], sk[6], sk[7], SIG3};
+    uint32_t y[16];
+    memcpy(y, in, sizeof y);
+    host_salsa_rounds(y);
+    for (int i = 0; i < 8; i++) (b ? p.k1024 : p.k0)[i] = y[i] + in[i];
+  }
+}
+
 hipError_t launch_crypt_fused(bool seal, const KeyArg& key, const NonceArg& bounds, const xs_block_desc* desc,
                               const xs_block_desc* host_desc, uint64_t nblocks, const uint8_t* src, uint8_t* dst,
                               uint8_t* ok, uint32_t* ctr, uint32_t* flag, uint32_t seq, hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
+  static const uint64_t pre_max = [] {  // env XS_KEY_PRE_MAX overrides (A/B, 0 = never)
+    const char* v = getenv("XS_KEY_PRE_MAX");
+    return std::min<uint64_t>(v ? strtoull(v, nullptr, 10) : (uint64_t)XS_KEY_PRE, (uint64_t)XS_KEY_PRE);
+  }();
   XsInlineDescs inl{};
   if (host_desc && nblocks <= (uint64_t)XS_INLINE_DESCS) {
     for (uint64_t i = 0; i < nblocks; i++) inl.d[i] = host_desc[i];
     inl.n = (uint32_t)nblocks;
+    // every block or none: the launch lasts as long as its slowest workgroup
+    if (nblocks <= pre_max) {
+      for (uint64_t i = 0; i < nblocks; i++) host_key_pre(key, host_desc[i].nonce, inl.pre[i]);
+      inl.npre = (uint32_t)nblocks;
+    }
   }
   // eight crypt waves (two per SIMD) + the key-schedule wave
   if (seal) hipLaunchKernelGGL((xs_crypt_fused2<true, 8>), dim3((unsigned)nblocks), dim3(576), 0, stream, key, bounds, desc, inl, nblocks, src, dst, ok, ctr, flag, seq);

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-5 A/B (recorded in DESIGN.md section 3e; the VALU kernel is profiles/r05/fused_vpoly/vpoly_kernel.patch, not kept).
+# Round-5 A/Bs of the fused kernel: the VALU tag alone (profiles/r05/fused_vpoly/vpoly_kernel.patch)
+# and the kept design (VALU tag for windowed opens + host key setup, profiles/r05/ranged_hybrid/).
 # Fused small-batch kernel, VALU Poly1305 (this tree, with that patch applied) against the matrix-core tag (tools/ab_old/:
 # the previous library and a seek_latency linked to it with RUNPATH $ORIGIN), on one box:
 # parity tests of the fused / ranged / engine paths first, then ranged reads alternating
