@@ -64,7 +64,7 @@ def _construct(cls, *a, **kw):
 def test_decrypter_sequences_match_reference(batch):
     rng = random.Random(0xDEC0 + batch)
     cases = ops_run = 0
-    for case in range(70):
+    for case in range(400):
         size = _size(rng)
         plain = bytes(rng.getrandbits(8) for _ in range(min(size, 64))) * (size // 64 + 1)
         plain = plain[:size]
