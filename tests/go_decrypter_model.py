@@ -1,9 +1,13 @@
-"""TEST INFRASTRUCTURE: a step-by-step Python restatement of the reference's decrypter state
-machine (backend/crypt/cipher.go:776-1087), used as the checker for randomised operation
-sequences on the GPU decrypter (tests/test_decrypter_fuzz_gpu.py).  Blocks are opened with the
-CPU oracle (oracle/pyoracle.py, secretbox.Open); nothing here is part of the product path.
+"""TEST INFRASTRUCTURE: step-by-step Python restatements of the reference's decrypter and
+encrypter state machines (backend/crypt/cipher.go:681-1087), used as the checkers for randomised
+operation sequences on the GPU decrypter and encrypter (tests/test_decrypter_fuzz_gpu.py).  Blocks
+are sealed and opened with the CPU oracle (oracle/pyoracle.py, secretbox.Seal / Open); nothing
+here is part of the product path.
 
 Followed line by line:
+  newEncrypter       cipher.go:694-716  (header = magic + nonce, served first)
+  encrypter.Read     cipher.go:719-745  (ReadFill of one block; n == 0 -> finish(err); Seal; increment)
+  encrypter.finish   cipher.go:748-758
   newDecrypterSeek   cipher.go:821-859  (open the header only, the header + limit, or the whole file)
   newDecrypter       cipher.go:793-818  (ReadFill of the 32-byte header, magic, nonce)
   fillBuffer         cipher.go:862-898  (ReadFill of one block, header check, Open, nonce.increment)
@@ -38,6 +42,32 @@ def _read_fill(r, n):
 
 class SeekStartError(crypt.CryptError):
     pass
+
+
+class ModelEncrypter:
+    """newEncrypter(in, nonce) + Read (cipher.go:694-758)."""
+
+    def __init__(self, key, src, nonce):
+        self.key, self.src, self.nonce = bytes(key), src, bytes(nonce)
+        self.buf = MAGIC + self.nonce  # bufSize = fileHeaderSize, bufIndex 0
+        self.idx = 0
+        self.err = None
+
+    def read_go(self, n):
+        if self.err is not None:
+            return b"", self.err
+        if self.idx >= len(self.buf):
+            data, err = _read_fill(self.src, BLOCK_DATA)
+            if not data:
+                if self.err is None:  # finish (cipher.go:748-758)
+                    self.err = err
+                return b"", self.err
+            self.buf = orc.seal(data, self.nonce, self.key)  # possibly err != nil: the next fill returns it
+            self.idx = 0
+            self.nonce = orc.nonce_increment(self.nonce)
+        out = self.buf[self.idx:self.idx + n]
+        self.idx += len(out)
+        return out, None
 
 
 class ModelDecrypter:

@@ -18,7 +18,7 @@ import pytest
 from oracle import pyoracle as orc
 from rclone_amd import crypt
 from rclone_amd.crypt import EOF
-from tests.go_decrypter_model import ModelDecrypter, kind
+from tests.go_decrypter_model import ModelDecrypter, ModelEncrypter, kind
 from tests.go_readers import Buffer
 
 torch = pytest.importorskip("torch")
@@ -121,3 +121,90 @@ def test_decrypter_sequences_match_reference(batch):
         with pytest.raises(crypt.ErrorFileClosed):
             gpu.close()
     print(f"batch {batch}: {cases} handles, {ops_run} calls matched the reference's state machine")
+
+
+class _ChunkSource:
+    """A Go io.Reader over `data` handing out random-size pieces (its own seeded stream, so two
+    instances behave alike), ending as `tail` says: "eof" ((0, EOF) after the data), "eof_with_data"
+    (the last piece comes with EOF), or an error value returned after the data (and again after)."""
+
+    def __init__(self, data, seed, tail):
+        self.data, self.pos, self.rng, self.tail = data, 0, random.Random(seed), tail
+
+    def read_go(self, n):
+        if self.pos >= len(self.data):
+            return b"", (EOF if self.tail in ("eof", "eof_with_data") else self.tail)
+        k = min(n, self.rng.choice([1, 17, 4096, 65536, 70000, self.rng.randrange(1, 100000)]))
+        out = self.data[self.pos:self.pos + k]
+        self.pos += len(out)
+        if self.tail == "eof_with_data" and self.pos >= len(self.data):
+            return out, EOF
+        return out, None
+
+
+class _Potato(Exception):
+    pass
+
+
+@pytest.mark.parametrize("batch", [1, 3, 64])
+def test_encrypter_sequences_match_reference(batch):
+    """EncryptData (cipher.go:694-758) call by call: random sources (piece sizes, io.EOF alone or
+    with the last piece, a reader error or io.ErrUnexpectedEOF after the data), random Read sizes,
+    the put tee MD5 on or off; bytes, errors and the tee digest equal the encrypter model's."""
+    import hashlib
+    rng = random.Random(0xE9C0 + batch)
+    calls = 0
+    spans = [0]  # calls whose bytes crossed a block boundary
+    joint = [0]  # calls that returned bytes and the stream's end together (the reference never does)
+
+    def model_block_rest(n, before):
+        # bytes left in the reference's current buffer (header, then 65552-byte blocks) at offset len(before)
+        pos = len(before)
+        if pos < 32:
+            return b"x" * (32 - pos)
+        return b"x" * (65552 - (pos - 32) % 65552)
+    for case in range(300):
+        size = _size(rng)
+        plain = bytes(rng.getrandbits(8) for _ in range(min(size, 64))) * (size // 64 + 1)
+        plain = plain[:size]
+        nonce = bytes(rng.getrandbits(8) for _ in range(24))
+        if case % 5 == 0:
+            nonce = b"\xff" * 8 + nonce[8:]
+        tail = rng.choice(["eof", "eof", "eof_with_data", _Potato("potato"), crypt.ErrUnexpectedEOF("unexpected EOF")])
+        seed = rng.getrandbits(32)
+        c = crypt.Cipher("", "", batch_blocks=batch)
+        gpu = c.encrypt_data(_ChunkSource(plain, seed, tail), nonce=nonce)
+        model = ModelEncrypter(bytes(32), _ChunkSource(plain, seed, tail), nonce)
+        tee = rng.random() < 0.5
+        if tee:
+            gpu.set_md5(True)
+        got_all = bytearray()
+        for step in range(200):
+            n = rng.choice([1, 7, 31, 4096, 65552, 70000, rng.randrange(1, 150000)])
+            got, gerr = gpu.read_go(n)
+            # The reference's Read returns at most the rest of one block per call; the library may hand
+            # out several buffered blocks at once (same stream, fewer calls).  The model is read up to
+            # the same byte count, and when the library ends the stream the model's next Read must
+            # give no bytes and the same error.
+            want, merr = b"", None
+            while len(want) < len(got) and merr is None:
+                d, merr = model.read_go(len(got) - len(want))
+                want += d
+            if gerr is not None and merr is None:
+                d, merr = model.read_go(n)
+                want += d
+            calls += 1
+            spans[0] += len(got) > len(model_block_rest(len(want), got_all))
+            joint[0] += bool(got) and gerr is not None
+            assert (got == want, kind(gerr)) == (True, kind(merr)), (case, size, tail, step, n, len(got), len(want),
+                                                                     gerr, merr)
+            got_all += got
+            if merr is not None:
+                break
+        assert merr is not None, (case, "stream did not end")
+        if tee:
+            assert gpu.md5() == hashlib.md5(bytes(got_all)).digest(), case
+    print(f"batch {batch}: 300 encrypters, {calls} calls matched the reference's stream and errors "
+          f"({spans[0]} of them crossed a block boundary and {joint[0]} returned bytes with the end, which "
+          "the reference's Read never does)")
+    assert joint[0] == 0  # bytes and the error of one Read come apart, as the reference's

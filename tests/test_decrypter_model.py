@@ -4,7 +4,10 @@ test, pinned to the reference's own decrypter tests before it is trusted:
   trial grid reads exactly plaintext[offset:offset+limit] on a fresh handle and after RangeSeek on
   one handle, and the open callback gets the reference's (offset, limit) pairs (:1367-1404);
 * TestDecrypterRead (cipher_test.go:1485-1560): file16 truncated to every length and with every
-  byte flipped gives the reference's error at the reference's point.
+  byte flipped gives the reference's error at the reference's point;
+and the encrypter model to TestEncryptData (cipher_test.go:1142-1171: file0 / file1 / file16
+byte for byte) and TestNewEncrypterErrUnexpectedEOF (:1194-1205: the 32-byte header, then the
+reader's io.ErrUnexpectedEOF).
 """
 import pytest
 
@@ -12,8 +15,8 @@ from oracle import pyoracle as orc
 from rclone_amd import crypt
 from rclone_amd.crypt import EOF
 from rclone_amd.testdata import random_source
-from tests.go_decrypter_model import ModelDecrypter, kind
-from tests.go_readers import Buffer, read_all
+from tests.go_decrypter_model import ModelDecrypter, ModelEncrypter, kind
+from tests.go_readers import Buffer, ErrorReader, read_all
 
 ZERO_KEY = bytes(32)
 
@@ -111,3 +114,12 @@ def test_model_edges():
     assert kind(err) == "can only seek from the start"
     assert kind(fh.range_seek(1, 0, -1)[1]) == "can only seek from the start"
     assert fh.close() is None and kind(fh.close()) == "ErrorFileClosed"
+
+
+def test_model_encrypter(ref_kat):
+    n0 = bytes(range(1, 25))  # randomSource's first 24 bytes (cipher_test.go:1153)
+    for name, plain in (("file0", b""), ("file1", b"\x01"), ("file16", bytes(range(1, 17)))):
+        assert read_all(ModelEncrypter(ZERO_KEY, Buffer(plain), n0), 7) == (bytes.fromhex(ref_kat[name]), None), name
+    fh = ModelEncrypter(ZERO_KEY, ErrorReader(crypt.ErrUnexpectedEOF("unexpected EOF")), n0)
+    out, err = read_all(fh)
+    assert len(out) == 32 and kind(err) == "ErrUnexpectedEOF"
