@@ -22,6 +22,10 @@
 //              multipliers r inside a group, r^253 between groups, final r^e from the
 //              tables; the 64 partial sums added with wave shuffles).  Lane 0 adds s and
 //              writes (seal) or checks (open) the tag.
+//   xs_crypt_fused2  tiny batches (ranged reads): one workgroup per block, key schedule and crypt
+//              in one launch.  A ranged read's open (a group window) computes its tag on the VALU
+//              from a 64-entry power table, with the key setup of one- and two-block launches
+//              derived on the host; whole blocks keep the matrix-core tag.
 //   Poly1305 arithmetic is radix 2^26 (5 limbs): the product columns are
 //   v_mad_u64_u32 chains, which measured as fast as v_alignbit on gfx950.
 //
