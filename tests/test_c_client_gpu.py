@@ -19,7 +19,8 @@ ones with the 192-bit nonce carry included.  Checks:
 every case at once over the one shared cipher (the Go side's --transfers goroutines calling
 through the shim concurrently; every thread's bytes and digests must equal thread 0's).  CPU
 suite: the same client over the host C++ with the GPU replaced by the CPU oracle
-(tests/native/stub_engine.cpp, test-only), under ASan + UBSan, with 3 threads.
+(tests/native/stub_engine.cpp, test-only), under ASan + UBSan with 3 threads, and under
+ThreadSanitizer with 4.
 """
 import hashlib
 import os
@@ -56,7 +57,7 @@ def _cases(ref_kat, sodium_vectors, sodium_pick):
     return [(bytes(32), ref), (bytes.fromhex(sodium_vectors["key"]), sod)]
 
 
-def _run_group(exe, tmp_path, tag, key, cases, timeout, threads=1):
+def _run_group(exe, tmp_path, tag, key, cases, timeout, threads=1, extra_env=None):
     manifest = tmp_path / f"{tag}.manifest"
     lines = [key.hex()]
     for i, (nonce, plain, *_rest) in enumerate(cases):
@@ -66,6 +67,7 @@ def _run_group(exe, tmp_path, tag, key, cases, timeout, threads=1):
     manifest.write_text("\n".join(lines) + "\n")
     env = dict(os.environ)
     env.setdefault("ASAN_OPTIONS", "detect_leaks=0")
+    env.update(extra_env or {})
     r = subprocess.run([exe, str(manifest), str(threads)], capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert r.stdout.rstrip().endswith("c client gpu ok")
@@ -117,6 +119,17 @@ def test_shim_data_path_cpu_stub(stub_client, tmp_path, ref_kat, sodium_vectors)
                           if f["plain"] == "splitmix64" and (f["size"] > 131072 or f["size"] in (0, 17, 65536))]
     for tag, (key, cases) in zip(("ref", "sod"), _cases(ref_kat, sodium_vectors, pick)):
         _run_group(stub_client, tmp_path, tag, key, cases, timeout=300, threads=3)
+
+
+def test_shim_data_path_cpu_stub_tsan(tmp_path, ref_kat, sodium_vectors):
+    """The same with 4 client threads under ThreadSanitizer: the shim's handle tables, the shared
+    cipher and the per-handle state touched from several threads at once (go test -race's role)."""
+    subprocess.check_call(["make", "-s", "-C", NATIVE, "build/c_client_stub_tsan"])
+    exe = os.path.join(NATIVE, "build", "c_client_stub_tsan")
+    pick = lambda files: [i for i, f in enumerate(files)  # noqa: E731
+                          if f["plain"] == "splitmix64" and f["size"] in (0, 17, 65536, 65537) or f["size"] > 196608]
+    for tag, (key, cases) in zip(("ref", "sod"), _cases(ref_kat, sodium_vectors, pick)):
+        _run_group(exe, tmp_path, tag, key, cases, timeout=600, threads=4, extra_env={"TSAN_OPTIONS": "halt_on_error=1"})
 
 
 @pytest.mark.gpu
