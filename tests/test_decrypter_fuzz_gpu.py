@@ -11,6 +11,7 @@ restatement of backend/crypt/cipher.go:776-1087 that tests/test_decrypter_model.
 reference's own decrypter tests.  Construction errors (the header, a seek past the end) must
 match too, and Close must close once.
 """
+import os
 import random
 
 import pytest
@@ -26,6 +27,9 @@ pytestmark = pytest.mark.gpu
 
 BLOCK_DATA = 65536
 BLOCK_SIZE = 65552
+# longer soaks: RCLONE_AMD_FUZZ_SCALE multiplies the case counts, RCLONE_AMD_FUZZ_SEED shifts the seeds
+SCALE = int(os.environ.get("RCLONE_AMD_FUZZ_SCALE", "1"))
+SEED = int(os.environ.get("RCLONE_AMD_FUZZ_SEED", "0"))
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -62,9 +66,9 @@ def _construct(cls, *a, **kw):
 
 @pytest.mark.parametrize("batch", [1, 3, 64])
 def test_decrypter_sequences_match_reference(batch):
-    rng = random.Random(0xDEC0 + batch)
+    rng = random.Random(0xDEC0 + batch + (SEED << 16))
     cases = ops_run = 0
-    for case in range(400):
+    for case in range(400 * SCALE):
         size = _size(rng)
         plain = bytes(rng.getrandbits(8) for _ in range(min(size, 64))) * (size // 64 + 1)
         plain = plain[:size]
@@ -152,7 +156,7 @@ def test_encrypter_sequences_match_reference(batch):
     with the last piece, a reader error or io.ErrUnexpectedEOF after the data), random Read sizes,
     the put tee MD5 on or off; bytes, errors and the tee digest equal the encrypter model's."""
     import hashlib
-    rng = random.Random(0xE9C0 + batch)
+    rng = random.Random(0xE9C0 + batch + (SEED << 16))
     calls = 0
     spans = [0]  # calls whose bytes crossed a block boundary
     joint = [0]  # calls that returned bytes and the stream's end together (the reference never does)
@@ -163,7 +167,7 @@ def test_encrypter_sequences_match_reference(batch):
         if pos < 32:
             return b"x" * (32 - pos)
         return b"x" * (65552 - (pos - 32) % 65552)
-    for case in range(300):
+    for case in range(300 * SCALE):
         size = _size(rng)
         plain = bytes(rng.getrandbits(8) for _ in range(min(size, 64))) * (size // 64 + 1)
         plain = plain[:size]
@@ -204,7 +208,7 @@ def test_encrypter_sequences_match_reference(batch):
         assert merr is not None, (case, "stream did not end")
         if tee:
             assert gpu.md5() == hashlib.md5(bytes(got_all)).digest(), case
-    print(f"batch {batch}: 300 encrypters, {calls} calls matched the reference's stream and errors "
+    print(f"batch {batch}: {300 * SCALE} encrypters, {calls} calls matched the reference's stream and errors "
           f"({spans[0]} of them crossed a block boundary and {joint[0]} returned bytes with the end, which "
           "the reference's Read never does)")
     assert joint[0] == 0  # bytes and the error of one Read come apart, as the reference's
