@@ -64,11 +64,10 @@ def _construct(cls, *a, **kw):
         return None, e
 
 
-@pytest.mark.parametrize("batch", [1, 3, 64])
-def test_decrypter_sequences_match_reference(batch):
-    rng = random.Random(0xDEC0 + batch + (SEED << 16))
+def _decrypter_run(rng, ncases, batch):
+    """ncases random handles, each with a random call sequence, against the model; (handles, calls)."""
     cases = ops_run = 0
-    for case in range(400 * SCALE):
+    for case in range(ncases):
         size = _size(rng)
         plain = bytes(rng.getrandbits(8) for _ in range(min(size, 64))) * (size // 64 + 1)
         plain = plain[:size]
@@ -124,7 +123,36 @@ def test_decrypter_sequences_match_reference(batch):
         assert model.close() is None
         with pytest.raises(crypt.ErrorFileClosed):
             gpu.close()
+    return cases, ops_run
+
+
+@pytest.mark.parametrize("batch", [1, 3, 64])
+def test_decrypter_sequences_match_reference(batch):
+    cases, ops_run = _decrypter_run(random.Random(0xDEC0 + batch + (SEED << 16)), 400 * SCALE, batch)
     print(f"batch {batch}: {cases} handles, {ops_run} calls matched the reference's state machine")
+
+
+def test_decrypter_sequences_concurrent():
+    """The same sequences from 8 threads at once (rclone's --transfers / multi-thread streams): the
+    handles share the device engine, whose coalescing queue and fused ranged opens then serve
+    several callers' refills together; every call must still equal its own model's."""
+    import threading
+    nthreads, results, errors = 8, {}, []
+
+    def worker(t):
+        try:
+            results[t] = _decrypter_run(random.Random(0xC0DE0 + t + (SEED << 16)), 60 * SCALE, (1, 3, 64)[t % 3])
+        except BaseException as exc:  # noqa: BLE001 -- reported below with its thread
+            errors.append((t, repr(exc)[:2000]))
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errors, errors
+    assert sorted(results) == list(range(nthreads))
+    print(f"{nthreads} threads: {sum(c for c, _ in results.values())} handles, "
+          f"{sum(o for _, o in results.values())} calls matched the reference's state machine")
 
 
 class _ChunkSource:
