@@ -136,23 +136,9 @@ def test_decrypter_sequences_concurrent():
     """The same sequences from 8 threads at once (rclone's --transfers / multi-thread streams): the
     handles share the device engine, whose coalescing queue and fused ranged opens then serve
     several callers' refills together; every call must still equal its own model's."""
-    import threading
-    nthreads, results, errors = 8, {}, []
-
-    def worker(t):
-        try:
-            results[t] = _decrypter_run(random.Random(0xC0DE0 + t + (SEED << 16)), 60 * SCALE, (1, 3, 64)[t % 3])
-        except BaseException as exc:  # noqa: BLE001 -- reported below with its thread
-            errors.append((t, repr(exc)[:2000]))
-    threads = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
-    for th in threads:
-        th.start()
-    for th in threads:
-        th.join()
-    assert not errors, errors
-    assert sorted(results) == list(range(nthreads))
-    print(f"{nthreads} threads: {sum(c for c, _ in results.values())} handles, "
-          f"{sum(o for _, o in results.values())} calls matched the reference's state machine")
+    res = _threads(8, lambda t: _decrypter_run(random.Random(0xC0DE0 + t + (SEED << 16)), 60 * SCALE, (1, 3, 64)[t % 3]))
+    print(f"8 threads: {sum(c for c, _ in res.values())} handles, "
+          f"{sum(o for _, o in res.values())} calls matched the reference's state machine")
 
 
 class _ChunkSource:
@@ -178,24 +164,18 @@ class _Potato(Exception):
     pass
 
 
-@pytest.mark.parametrize("batch", [1, 3, 64])
-def test_encrypter_sequences_match_reference(batch):
-    """EncryptData (cipher.go:694-758) call by call: random sources (piece sizes, io.EOF alone or
-    with the last piece, a reader error or io.ErrUnexpectedEOF after the data), random Read sizes,
-    the put tee MD5 on or off; bytes, errors and the tee digest equal the encrypter model's."""
-    import hashlib
-    rng = random.Random(0xE9C0 + batch + (SEED << 16))
-    calls = 0
-    spans = [0]  # calls whose bytes crossed a block boundary
-    joint = [0]  # calls that returned bytes and the stream's end together (the reference never does)
+def _block_rest(pos):
+    """Bytes left in the reference encrypter's current buffer (the header, then 65552-byte blocks)
+    at stream offset pos: the most one of its Reads returns there."""
+    return 32 - pos if pos < 32 else 65552 - (pos - 32) % 65552
 
-    def model_block_rest(n, before):
-        # bytes left in the reference's current buffer (header, then 65552-byte blocks) at offset len(before)
-        pos = len(before)
-        if pos < 32:
-            return b"x" * (32 - pos)
-        return b"x" * (65552 - (pos - 32) % 65552)
-    for case in range(300 * SCALE):
+
+def _encrypter_run(rng, ncases, batch):
+    """ncases random encrypters read with random sizes against the model; (calls, calls crossing a
+    block boundary, calls returning bytes together with the stream's end)."""
+    import hashlib
+    calls = spans = joint = 0
+    for case in range(ncases):
         size = _size(rng)
         plain = bytes(rng.getrandbits(8) for _ in range(min(size, 64))) * (size // 64 + 1)
         plain = plain[:size]
@@ -226,8 +206,8 @@ def test_encrypter_sequences_match_reference(batch):
                 d, merr = model.read_go(n)
                 want += d
             calls += 1
-            spans[0] += len(got) > len(model_block_rest(len(want), got_all))
-            joint[0] += bool(got) and gerr is not None
+            spans += len(got) > _block_rest(len(got_all))
+            joint += bool(got) and gerr is not None
             assert (got == want, kind(gerr)) == (True, kind(merr)), (case, size, tail, step, n, len(got), len(want),
                                                                      gerr, merr)
             got_all += got
@@ -236,7 +216,45 @@ def test_encrypter_sequences_match_reference(batch):
         assert merr is not None, (case, "stream did not end")
         if tee:
             assert gpu.md5() == hashlib.md5(bytes(got_all)).digest(), case
+    return calls, spans, joint
+
+
+@pytest.mark.parametrize("batch", [1, 3, 64])
+def test_encrypter_sequences_match_reference(batch):
+    """EncryptData (cipher.go:694-758) call by call: random sources (piece sizes, io.EOF alone or
+    with the last piece, a reader error or io.ErrUnexpectedEOF after the data), random Read sizes,
+    the put tee MD5 on or off; bytes, errors and the tee digest equal the encrypter model's."""
+    calls, spans, joint = _encrypter_run(random.Random(0xE9C0 + batch + (SEED << 16)), 300 * SCALE, batch)
     print(f"batch {batch}: {300 * SCALE} encrypters, {calls} calls matched the reference's stream and errors "
-          f"({spans[0]} of them crossed a block boundary and {joint[0]} returned bytes with the end, which "
+          f"({spans} of them crossed a block boundary and {joint} returned bytes with the end, which "
           "the reference's Read never does)")
-    assert joint[0] == 0  # bytes and the error of one Read come apart, as the reference's
+    assert joint == 0  # bytes and the error of one Read come apart, as the reference's
+
+
+def _threads(nthreads, fn):
+    """fn(t) on nthreads threads at once; {t: result}, any thread's exception re-raised here."""
+    import threading
+    results, errors = {}, []
+
+    def worker(t):
+        try:
+            results[t] = fn(t)
+        except BaseException as exc:  # noqa: BLE001 -- reported below with its thread
+            errors.append((t, repr(exc)[:2000]))
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errors, errors
+    assert sorted(results) == list(range(nthreads))
+    return results
+
+
+def test_encrypter_sequences_concurrent():
+    """The encrypter sequences from 8 threads at once: seals and tee MD5s of concurrent uploads
+    meet in the shared engine and the MD5 workers; every stream, error and digest equal its model's."""
+    res = _threads(8, lambda t: _encrypter_run(random.Random(0xC0E0 + t + (SEED << 16)), 40 * SCALE, (1, 3, 64)[t % 3]))
+    assert all(j == 0 for _, _, j in res.values())
+    print(f"8 threads: {40 * SCALE * 8} encrypters, {sum(c for c, _, _ in res.values())} calls matched the "
+          "reference's stream and errors")
