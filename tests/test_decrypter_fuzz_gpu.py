@@ -9,7 +9,9 @@ ranged opens that decrypt only the 4 KiB groups a limit reaches, pass_bad_blocks
 call by call, the same bytes and the same error as tests/go_decrypter_model.py, the step-by-step
 restatement of backend/crypt/cipher.go:776-1087 that tests/test_decrypter_model.py pins to the
 reference's own decrypter tests.  Construction errors (the header, a seek past the end) must
-match too, and Close must close once.
+match too, and Close must close once.  The encrypter gets the same treatment against
+ModelEncrypter.  Both also run from 8 threads at once over the shared engine, and
+RCLONE_AMD_FUZZ_SCALE / RCLONE_AMD_FUZZ_SEED turn any of them into a longer soak.
 """
 import os
 import random
