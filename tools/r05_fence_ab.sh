@@ -4,7 +4,8 @@
 # linked to it with RUNPATH $ORIGIN; tools/microbench/launch_word_old built from the previous kernel
 # file).  Parity tests of the fused / ranged / engine / shim paths and the fuzz first, then launch ->
 # completion word (windowed and whole-block opens, host key setup, high-priority stream) and 4 KiB
-# ranged reads through DecryptDataSeek (1 and 16 readers), alternating new / old.
+# ranged reads through DecryptDataSeek (1 and 16 readers), alternating new / old; PROF_BOTH=1 adds a
+# kernel trace of one 4 KiB run of each.  Also used for the even-split A/B (profiles/r05/even_split/).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${1:-r05_fence}
@@ -41,4 +42,5 @@ for f in ("seek.jsonl", "seek16.jsonl"):
         x = json.loads(l); r = x["seek"]
         print(f, x["lib"], "pair", x["pair"], "p50", r["p50_us"], "p90", r["p90_us"], "p99", r["p99_us"], "reads/s", r["reads_per_s"], "bad", r["bad"])
 PY
+if [ -n "$PROF_BOTH" ]; then export TMPDIR=/tmp; for v in new old; do if [ $v = old ]; then E=$R/tools/microbench/ab_prev/seek_latency_old; else E=$R/tools/seek_latency; fi; (cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$v -o run -- $E --mib 256 --reads 2000 --len 4096 --threads 1 > $OUT/prof_$v.json 2>&1) || { echo PROF_FAILED $v; exit 1; }; done; for f in $(find $OUT/prof_new $OUT/prof_old -name "*kernel_stats.csv"); do echo "== $f"; python3 -c "import csv,sys; [print(r[\"Name\"][:50], r[\"Calls\"], round(float(r[\"AverageNs\"])/1000, 2), \"us\") for r in csv.DictReader(open(sys.argv[1])) if \"fused\" in r[\"Name\"]]" $f; done; fi
 echo FENCE_AB_DONE
