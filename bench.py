@@ -39,8 +39,15 @@ BLOCK_SIZE = 65552
 # (the 960-byte per-block key schedule is this design's own intermediate, not counted)
 ALG_BYTES_SEAL = 65536 + 65552
 ALG_BYTES_OPEN = 65552 + 65536 + 1
+READ_BYTES_SEAL, READ_BYTES_OPEN = 65536, 65552  # the read half alone (SURVEY 8(d) "HBM-read roofline")
 VALU_CYC, SIMDS, CLOCK_HZ = 4, 256 * 4, 2.4e9
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# the headline resident set: global block g = SplitMix64(HEADLINE_SEED) block g, sealed with
+# HEADLINE_NONCE0 + g (the nonce carries across byte 8 inside the set); its tag digest for 1/2/4/8
+# ranks is pinned by the CPU oracle in tests/golden/fullsize.json (tests/golden/make_fullsize.py)
+HEADLINE_KEY = bytes(range(32))
+HEADLINE_NONCE0 = bytes([0xF0]) + bytes([0xFF] * 7) + bytes(16)
+HEADLINE_SEED = 0x5EED
 
 
 def parse():
@@ -181,17 +188,38 @@ def run_dry(args, world, rank, dist):
     """--dry-run: the launch and the collective without any device work (CPU test of N > 1)."""
     import torch
     seen = dist.get_world_size() if grouped(world) else 1
-    t = torch.tensor([1, rank], dtype=torch.int64)
+    # a stand-in for a shard's digest contribution (rank + 1); BENCH_FORCE_DIGEST_MISMATCH=1 makes
+    # rank BENCH_FORCE_FAIL_RANK (default the last) contribute a wrong one, as a bad shard would:
+    # the summed digest then misses on every rank and the run must end non-zero, as the real leg's
+    forced = os.environ.get("BENCH_FORCE_DIGEST_MISMATCH") == "1" and \
+        rank == int(os.environ.get("BENCH_FORCE_FAIL_RANK", world - 1))
+    t = torch.tensor([1, rank, rank + 1 + int(forced)], dtype=torch.int64)
     if grouped(world):
         dist.all_reduce(t)
+    objset_ok = int(t[2]) == world * (world + 1) // 2
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "dry_run": True,
                           "config": {"ranks_seen": seen, "ranks_reported": int(t[0]), "rank_sum": int(t[1]),
-                                     "process_group": dist.get_backend() if grouped(world) else None}}),
+                                     "process_group": dist.get_backend() if grouped(world) else None},
+                          "objectset": {"ok": objset_ok, "digest_stand_in": int(t[2])}}),
               flush=True)
     if grouped(world):
         dist.destroy_process_group()
+    fail_if_wrong(True, None, None, 0, objset_ok)
+
+
+def fail_if_wrong(digest_ok, digest, expect, tag_failures, objset_ok):
+    """End the run non-zero (after the line is printed) when a result is wrong: the headline set's
+    tag digest differs from the CPU oracle's, a headline tag failed, or the configs[3] leg failed.
+    Every rank calls it with the same, already all-reduced, inputs, so every rank exits non-zero."""
+    bad = [] if digest_ok else [f"headline tag digest {digest} != oracle {expect}"]
+    if tag_failures:
+        bad.append(f"{tag_failures} tag failures in the headline set")
+    if objset_ok is False:
+        bad.append("objectset leg failed (tag digest vs the oracle's, counters or tag failures)")
+    if bad:
+        raise SystemExit("bench: " + "; ".join(bad))
 
 
 def cpu_baseline(seconds):
@@ -284,6 +312,140 @@ class ClockProbe:
         return {"shader_clock_ghz": round((t1 - t0) / (r1 - r0) / 10.0, 4), "window_s": round((r1 - r0) / 1e8, 4),
                 "samples": n, "source": "xs_clock_probe_dev: s_memtime / s_memrealtime (100 MHz), one wave on a side "
                                        "stream over the first 80% of the timed steps"}
+
+
+class PowerSampler:
+    """Board power and shader clock over the timed window, read in-process from the rank's amdgpu
+    hwmon directory in sysfs (no child process, no GPU call): a thread samples power1_average
+    (else power1_input; microwatts) and freq1_input (sclk, Hz) every `period` seconds between
+    start() and stop().  When energy1_input (microjoules, a running counter) exists, energy is
+    its difference over the window; otherwise the mean sampled power x the window.  Every figure
+    is None when the directory or the file is absent (e.g. a container without the device)."""
+
+    def __init__(self, pci, period=0.005):
+        import glob
+        import threading
+        self.threading, self.period = threading, period
+        self.dir = None
+        dom, bus, dv = pci
+        for d in sorted(glob.glob(f"/sys/bus/pci/devices/{dom:04x}:{bus:02x}:{dv:02x}.0/hwmon/hwmon*")):
+            if any(os.path.exists(os.path.join(d, f)) for f in ("power1_average", "power1_input")):
+                self.dir = d
+                break
+        self.pfile = self._file("power1_average") or self._file("power1_input")
+        self.ffile = self._file("freq1_input")
+        self.efile = self._file("energy1_input")
+        self.p, self.f = [], []
+        self.t0 = self.t1 = self.e0 = self.e1 = None
+        self._stop = None
+
+    def _file(self, name):
+        if self.dir and os.path.exists(os.path.join(self.dir, name)):
+            return os.path.join(self.dir, name)
+        return None
+
+    @staticmethod
+    def _read(path):
+        try:
+            with open(path) as fh:
+                return int(fh.read().strip())
+        except (OSError, ValueError):
+            return None
+
+    def _loop(self):
+        while not self._stop.wait(self.period):
+            if self.pfile:
+                v = self._read(self.pfile)
+                if v is not None:
+                    self.p.append(v * 1e-6)
+            if self.ffile:
+                v = self._read(self.ffile)
+                if v is not None:
+                    self.f.append(v * 1e-9)
+
+    def start(self):
+        if not self.pfile:
+            return
+        self.e0 = self._read(self.efile) if self.efile else None
+        self._stop = self.threading.Event()
+        self._th = self.threading.Thread(target=self._loop, daemon=True)
+        self.t0 = time.perf_counter()
+        self._th.start()
+
+    def stop(self):
+        if not self._stop:
+            return
+        self.t1 = time.perf_counter()
+        self._stop.set()
+        self._th.join()
+        self.e1 = self._read(self.efile) if self.efile else None
+
+    def result(self):
+        """(mean W, joules over the window, mean sclk GHz, dict for the line) or Nones."""
+        if not self.p or self.t0 is None:
+            return None, None, (sum(self.f) / len(self.f) if self.f else None), \
+                {"source": "absent: no amdgpu hwmon power file for this GPU in sysfs"}
+        w = sum(self.p) / len(self.p)
+        span = self.t1 - self.t0
+        if self.e0 is not None and self.e1 is not None and self.e1 > self.e0:
+            joules, how = (self.e1 - self.e0) * 1e-6, "energy1_input difference"
+        else:
+            joules, how = w * span, f"mean of {len(self.p)} {os.path.basename(self.pfile)} samples x window"
+        ghz = sum(self.f) / len(self.f) if self.f else None
+        return w, joules, ghz, {"source": f"{self.dir} ({how})", "window_s": round(span, 4),
+                                "samples": len(self.p), "mean_W": round(w, 1), "min_W": round(min(self.p), 1),
+                                "max_W": round(max(self.p), 1),
+                                "sclk_ghz_mean": round(ghz, 4) if ghz else None}
+
+
+def energy_per_gib(rows, total_bytes):
+    """Whole-job joules over the timed window (summed over ranks) per GiB pushed through the cipher
+    (both directions counted, as `value`); None unless every rank had a power reading."""
+    js = [r[4] for r in rows]
+    if not js or any(j is None for j in js) or not total_bytes:
+        return None
+    return round(sum(js) / (total_bytes / 2**30), 4)
+
+
+def headline_expected_digest(world, nb, independent):
+    """The CPU oracle's tag digest of the headline set for this layout, or None when
+    tests/golden/fullsize.json does not pin it (another --blocks, --independent, another N)."""
+    if os.environ.get("BENCH_FORCE_DIGEST_MISMATCH") == "2":  # tests: a wrong headline digest fails the run
+        return "0" * 32
+    if independent:
+        return None
+    from rclone_amd.objectset import fullsize_pins
+    hl = fullsize_pins()["bench_headline"]
+    if (hl["blocks_per_rank"], hl["seed"], hl["key"], hl["nonce0"]) != (nb, HEADLINE_SEED, HEADLINE_KEY.hex(),
+                                                                        HEADLINE_NONCE0.hex()):
+        return None
+    return hl["tag_digest"].get(str(world))
+
+
+def per_rank(dist, world, rank, dev, values):
+    """Gather one row of floats per rank (one all-reduce of a world x k tensor; the row alone at
+    N = 1) -> list of rows, rank order."""
+    import torch
+    t = torch.zeros((world, len(values)), dtype=torch.float64, device=dev)
+    t[rank] = torch.tensor([float("nan") if v is None else float(v) for v in values], dtype=torch.float64)
+    if grouped(world):
+        # NaN (a rank without a reading) would poison the SUM: carry a mask beside the values
+        m = torch.isnan(t)
+        t[m] = 0.0
+        mask = (~m).to(torch.float64)
+        dist.all_reduce(t)
+        dist.all_reduce(mask)
+        t[mask == 0] = float("nan")
+    return [[None if x != x else x for x in row] for row in t.cpu().tolist()]
+
+
+def spread(col, nd=4):
+    """min / max / list of one per-rank column (Nones skipped)."""
+    xs = [x for x in col if x is not None]
+    if not xs:
+        return None
+    return {"min": round(min(xs), nd), "max": round(max(xs), nd), "per_rank": [None if x is None else round(x, nd)
+                                                                              for x in col]}
 
 
 def issue_bound(valu_insts, ms, clock_hz=None, mfma_insts=None):
@@ -460,25 +622,33 @@ def objectset_leg(args, world, rank, dev, dist):
     blocks, nbytes, fails, mism, d0, d1 = digest_to_u64(counters)
     digest = f"{d1:016x}{d0:016x}"  # the last pass's, summed over the ranks
     full = total == CONFIG3_BLOCKS
+    if os.environ.get("BENCH_FORCE_DIGEST_MISMATCH") == "1":  # tests: a wrong shard must fail the run
+        digest = "0" * 32
     ok = fails == 0 and mism == 0 and blocks == args.objectset_steps * total and (digest == CONFIG3_TAG_DIGEST or not full)
+    seal_avg = sum(seal_ms) / max(len(seal_ms), 1)
+    open_avg = sum(open_ms) / max(len(open_ms), 1)
+    rows = per_rank(dist, world, rank, dev, [seal_avg, open_avg, r.n])
     del r
     torch.cuda.empty_cache()
     if rank != 0:
-        return None
+        return None, ok
     return {"workload": f"BASELINE configs[3]: one {total}-block object ({total * BLOCK_DATA / 2**40:.3f} TiB) "
                         f"round-robin over {world} rank(s), {CONFIG3_ROUND_BLOCKS}-block rounds; one step = "
                         "generate in HBM + seal + open + verify every block",
             "value": round(2 * nbytes / 2**30 / el, 3), "unit": "GiB/s", "scaling": "strong",
             "steps": args.objectset_steps, "warmup": args.objectset_warmup,
             "ms_per_step": round(el / args.objectset_steps * 1e3, 3), "ok": ok,
-            "seal_kernel_ms_avg": round(sum(seal_ms) / max(len(seal_ms), 1), 4),
-            "open_kernel_ms_avg": round(sum(open_ms) / max(len(open_ms), 1), 4),
+            "seal_kernel_ms_avg": round(seal_avg, 4),
+            "open_kernel_ms_avg": round(open_avg, 4),
+            "per_rank": {"seal_kernel_ms": spread([x[0] for x in rows]), "open_kernel_ms": spread([x[1] for x in rows]),
+                         "blocks_per_pass": [int(x[2]) for x in rows]},
             "setup_s": round(setup_s, 2),
             "counters": {"blocks": blocks, "bytes": nbytes, "tag_failures": fails, "roundtrip_mismatch_words": mism,
                          "tag_digest": digest,
                          "tag_digest_expected": CONFIG3_TAG_DIGEST if full else None,
-                         "digest_source": "one pass, summed over ranks; expected = tests/test_objectset_gpu.py at world "
-                                          "1/2/8 (rclone_amd.objectset.CONFIG3_TAG_DIGEST)"}}
+                         "digest_source": "one pass, summed over ranks; expected = the CPU oracle's digest of all "
+                                          "2^24 blocks (tests/golden/fullsize.json config3, "
+                                          "tests/golden/make_fullsize.py)"}}, ok
 
 
 def run_objectset(args, world, rank, dev, dist):
@@ -859,8 +1029,7 @@ def main():
     nb = args.blocks
     plain_len = nb * BLOCK_DATA
     body_len = nb * BLOCK_SIZE
-    key = bytes(range(32))
-    nonce0 = bytes([0xF0]) + bytes([0xFF] * 7) + bytes(16)  # nonce carries cross byte 8 in the set
+    key, nonce0 = HEADLINE_KEY, HEADLINE_NONCE0
     # this rank's round-robin share of one logical object of world*nb blocks (BASELINE config 4
     # layout); per-block nonces via descriptors, blocks packed contiguously in local HBM
     gidx = shard.owned_blocks(world * nb, world, rank)
@@ -872,7 +1041,7 @@ def main():
     d_seal = torch.from_numpy(ds.view(np.uint8).copy()).to(dev)
     d_open = torch.from_numpy(do.view(np.uint8).copy()).to(dev)
     plain = torch.empty(plain_len, dtype=torch.uint8, device=dev)
-    device.fill_blocks(plain, rank, world, 0x5EED)  # global block g = rank + world*i, keyed by g
+    device.fill_blocks(plain, rank, world, HEADLINE_SEED)  # global block g = rank + world*i, keyed by g
     body = torch.empty(body_len, dtype=torch.uint8, device=dev)
     out = torch.empty(plain_len, dtype=torch.uint8, device=dev)
     ok = torch.empty(nb, dtype=torch.uint8, device=dev)
@@ -930,13 +1099,18 @@ def main():
         dist.barrier()
     # the clock probe runs at N=1 only (RCCL's own streams could share its hardware queue)
     probe = ClockProbe(L, dev) if world == 1 else None
+    props = torch.cuda.get_device_properties(dev)
+    power = PowerSampler((props.pci_domain_id, props.pci_bus_id, props.pci_device_id))
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     if probe:
         probe.start(0.8 * args.steps * step_s)
+    power.start()
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize(dev)
+    power.stop()
+    el_rank = time.perf_counter() - t0  # this rank's own steps (the straggler view)
     if grouped(world):
         dist.barrier()
     el = time.perf_counter() - t0
@@ -955,13 +1129,20 @@ def main():
     el = float(tmax.item())
     seal_ms = [a.elapsed_time(b) for s, a, b in ev if s]
     open_ms = [a.elapsed_time(b) for s, a, b in ev if not s]
+    seal_avg = sum(seal_ms) / len(seal_ms)
+    open_avg = sum(open_ms) / len(open_ms)
+    watts, joules, sclk, power_info = power.result()
+    rows = per_rank(dist, world, rank, dev, [el_rank, seal_avg, open_avg, watts, joules, sclk])
+    # the headline set's tag digest against the CPU oracle's (tests/golden/fullsize.json), for the
+    # layouts it pins: --blocks 100000 at 1/2/4/8 ranks, one object (not --independent)
+    digest = "%016x%016x" % (int(counters[4].item()) & (2**64 - 1), int(counters[3].item()) & (2**64 - 1))
+    expect = headline_expected_digest(world, nb, args.independent)
+    digest_ok = expect is None or digest == expect
     # configs[3] leg: every rank, after the headline's timing and reduction (never inside them)
-    objset = objectset_leg(args, world, rank, dev, dist) if args.objectset_steps > 0 else None
+    objset, objset_ok = objectset_leg(args, world, rank, dev, dist) if args.objectset_steps > 0 else (None, None)
     if os.environ.get("BENCH_TRACE"):
         print("seal_ms", [round(x, 3) for x in seal_ms], "\nopen_ms", [round(x, 3) for x in open_ms],
               file=sys.stderr)
-    seal_avg = sum(seal_ms) / len(seal_ms)
-    open_avg = sum(open_ms) / len(open_ms)
     total_bytes = int(counters[1].item())
     value = total_bytes / 2**30 / el
     if rank == 0:
@@ -1005,21 +1186,36 @@ def main():
                          "traffic": per("seal_bytes_per_launch"),
                          "kernel_ms_avg": round(seal_avg, 4),
                          "alg_bytes_per_launch": ALG_BYTES_SEAL * nb,
+                         # SURVEY 8(d)'s HBM-read roofline: the bytes the kernel must read (65536
+                         # plaintext per block) per second against the same 8 TB/s
+                         "read_achieved": round(READ_BYTES_SEAL * nb / (seal_avg * 1e-3) / 1e9, 1),
+                         "read_frac": round(READ_BYTES_SEAL * nb / (seal_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "traffic_source": tr.get("source") if tr else stale,
                          "traffic_git_head": tr.get("git_head"),
                          "valu": issue_bound(per("seal_valu_wave_insts_per_launch"), seal_avg, clk_hz,
                                              per("seal_mfma_wave_insts_per_launch")),
                          "open": {"kernel": "xs_open", "achieved": round(ach_open, 1),
                                   "frac": round(ach_open / HBM_PEAK_GBS, 4), "kernel_ms_avg": round(open_avg, 4),
+                                  "read_achieved": round(READ_BYTES_OPEN * nb / (open_avg * 1e-3) / 1e9, 1),
+                                  "read_frac": round(READ_BYTES_OPEN * nb / (open_avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                                     4),
                                   "traffic": per("open_bytes_per_launch"),
                                   "valu": issue_bound(per("open_valu_wave_insts_per_launch"), open_avg, clk_hz,
                                                       per("open_mfma_wave_insts_per_launch"))}},
             "clock": clock,
+            "energy_J_per_GiB": energy_per_gib(rows, total_bytes),
+            "power": power_info,
+            "per_rank": {"step_ms": spread([r[0] * 1e3 / args.steps for r in rows], 3),
+                         "seal_kernel_ms": spread([r[1] for r in rows]),
+                         "open_kernel_ms": spread([r[2] for r in rows]),
+                         "power_W": spread([r[3] for r in rows], 1),
+                         "sclk_ghz": spread([r[5] for r in rows])},
             "warmup_s": round(warm_s, 3), "warmup_steps": nwarm,
             "counters": {"blocks": int(counters[0].item()), "bytes": total_bytes,
                          "tag_failures": int(counters[2].item()),
-                         "tag_digest": "%016x%016x" % (int(counters[4].item()) & (2**64 - 1),
-                                                       int(counters[3].item()) & (2**64 - 1))},
+                         "tag_digest": digest, "tag_digest_expected": expect, "tag_digest_ok": digest_ok,
+                         "digest_source": "summed over ranks; expected = CPU oracle, tests/golden/fullsize.json "
+                                          "bench_headline (tests/golden/make_fullsize.py)"},
             "cpu_baseline": None,
             "objectset": objset,
         }
@@ -1033,6 +1229,7 @@ def main():
         if not args.no_pool_check:
             res["pool_check"] = pool_check()
         print(json.dumps(res), flush=True)
+    fail_if_wrong(digest_ok, digest, expect, int(counters[2].item()), objset_ok)
 
 
 if __name__ == "__main__":

@@ -56,6 +56,10 @@ def _load():
     lib.orc_simd_seal_blocks.restype = ctypes.c_int
     lib.orc_simd_open_blocks.argtypes = [vp, vp, vp, ctypes.c_int64, c_p, c_p]
     lib.orc_simd_open_blocks.restype = ctypes.c_int
+    lib.orc_gen_block.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
+    lib.orc_simd_seal_gen.argtypes = [vp, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, c_p, vp,
+                                      c_p, vp]
+    lib.orc_simd_seal_gen.restype = ctypes.c_int
     lib.orc_seal_desc.argtypes = [vp, vp, vp, ctypes.c_int64, c_p]
     lib.orc_seal_desc.restype = ctypes.c_int
     lib.orc_open_desc.argtypes = [vp, vp, vp, vp, ctypes.c_int64, c_p]
@@ -198,3 +202,28 @@ def pkcs7_unpad(b: bytes):
     if any(x != p for x in b[-p:]):
         return "ErrorPaddingNotAllTheSame"
     return b[:-p]
+
+
+# ------------------------------------------------------------------ generated object sets (xsalsa_simd.c)
+def gen_block(seed: int, g: int) -> bytes:
+    """Global 64 KiB block g of the SplitMix64 stream (what xs_fill_blocks_dev writes)."""
+    out = ctypes.create_string_buffer(BLOCK_DATA)
+    lib().orc_gen_block(out, seed, g)
+    return out.raw
+
+
+def seal_gen(nblocks: int, first: int, stride: int, seed: int, nonce0: bytes, key: bytes, out=None, nonces=None):
+    """Seal generated blocks g = first + j*stride (j < nblocks), block g with nonce0 + g, or with
+    nonces[j] (a C-contiguous u8 array of nblocks x 24) when given.
+    out: None (digest only) or a writable u8 numpy array of nblocks*65552 bytes for the wire blocks.
+    Returns ((tag sum lo, tag sum hi) mod 2^64, OpenMP threads)."""
+    if out is not None:
+        assert out.nbytes >= nblocks * BLOCK_SIZE
+    if nonces is not None:
+        assert nonces.dtype.itemsize == 1 and nonces.size == nblocks * 24 and nonces.flags.c_contiguous
+    s = (ctypes.c_uint64 * 2)()
+    threads = lib().orc_simd_seal_gen(None if out is None else out.ctypes.data, nblocks, first, stride, seed,
+                                      bytes(nonce0), None if nonces is None else nonces.ctypes.data, bytes(key), s)
+    if threads == 0:
+        raise RuntimeError("orc_simd_seal_gen needs AVX2")
+    return (int(s[0]), int(s[1])), threads

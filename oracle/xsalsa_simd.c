@@ -343,3 +343,67 @@ int orc_simd_open_blocks(uint8_t *out, uint8_t *ok, const uint8_t *in, int64_t n
   }
   return threads;
 }
+
+/* ------------------------------------------------------------------ generated object sets
+ * The synthetic objects of BASELINE configs[1] and configs[3] are generated in HBM by
+ * xs_fill_blocks_dev: 64-bit word w of global 64 KiB block g is SplitMix64 word g*8192 + w of
+ * (seed), i.e. mix(seed + (g*8192 + w + 1) * golden) (rclone_amd/testdata.py).  Block g is sealed
+ * with nonce0 + g (cipher.go:665-678 nonce.add, :737 secretbox.Seal).
+ *
+ * orc_simd_seal_gen regenerates that plaintext here for blocks g = first + j*stride (j < nblocks),
+ * seals each one, writes the wire blocks to out when out != NULL (j-th block at out + j*65552) and
+ * returns through tagsum[2] the order-independent tag digest the GPU harness reports: the sum mod
+ * 2^64 of each tag's two little-endian 64-bit halves (rclone_amd/objectset.py tag_digest).  With
+ * out == NULL nothing but the digest is kept, so a 1 TiB set (2^24 blocks) streams through 64 KiB
+ * per thread.  nonces != NULL replaces nonce0 + g by nonces[24 j..24 j+23] (one-block objects, each with
+ * its own nonce: configs[1]'s independent-object form).  Returns the OpenMP threads used, 0 when the
+ * CPU has no AVX2. */
+static inline uint64_t splitmix_word(uint64_t seed, uint64_t k) {
+  uint64_t z = seed + (k + 1) * 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+void orc_gen_block(uint8_t out[SB_DATA], uint64_t seed, uint64_t g) {
+  uint64_t w[SB_DATA / 8];
+  const uint64_t base = g * (SB_DATA / 8);
+  for (uint64_t i = 0; i < SB_DATA / 8; i++) w[i] = splitmix_word(seed, base + i);
+  memcpy(out, w, SB_DATA); /* little-endian host: word i -> bytes 8i..8i+7 */
+}
+
+int orc_simd_seal_gen(uint8_t *out, int64_t nblocks, uint64_t first, uint64_t stride, uint64_t seed,
+                      const uint8_t nonce0[24], const uint8_t *nonces, const uint8_t key[32], uint64_t tagsum[2]) {
+  const int level = orc_simd_level();
+  if (level == 0) return 0;
+  int threads = 1;
+  uint64_t s0 = 0, s1 = 0;
+#pragma omp parallel reduction(+ : s0, s1)
+  {
+#ifdef _OPENMP
+#pragma omp single
+    threads = omp_get_num_threads();
+#endif
+    uint8_t plain[SB_DATA] __attribute__((aligned(64)));
+    uint8_t wire[SB_SIZE] __attribute__((aligned(64)));
+#pragma omp for schedule(static)
+    for (int64_t j = 0; j < nblocks; j++) {
+      const uint64_t g = first + (uint64_t)j * stride;
+      uint8_t n[24];
+      if (nonces) {
+        memcpy(n, nonces + (size_t)j * 24, 24);
+      } else {
+        memcpy(n, nonce0, 24);
+        orc_nonce_add(n, g);
+      }
+      orc_gen_block(plain, seed, g);
+      uint8_t *dst = out ? out + (size_t)j * SB_SIZE : wire;
+      seal_one(dst, plain, SB_DATA, n, key, level);
+      s0 += le64(dst);
+      s1 += le64(dst + 8);
+    }
+  }
+  tagsum[0] = s0;
+  tagsum[1] = s1;
+  return threads;
+}

@@ -14,6 +14,8 @@ This is measurement/test harness code around the product kernels; it never falls
 CPU (every kernel call goes through librclone_crypt.so).
 """
 import ctypes
+import json
+import os
 
 import numpy as np
 import torch
@@ -32,10 +34,29 @@ CONFIG3_KEY = bytes(range(100, 132))
 CONFIG3_NONCE0 = b"\xf0" + b"\xff" * 7 + bytes(range(16))  # the set's nonces carry across byte 8
 CONFIG3_SEED = 0x1417
 CONFIG3_ROUND_BLOCKS = 100_000
-# the order-independent tag digest of one pass over that set (hi || lo, hex), measured on the GPU by
-# tests/test_objectset_gpu.py at world 1, 2 and 8 (equal for all three; each rank's last block is
-# checked against the CPU oracle there): a regression anchor for the test and the bench leg
-CONFIG3_TAG_DIGEST = "26763293cb7e88a920e9c78b28f3f58d"
+# Oracle pins of the full-size synthetic workloads (data, not code): computed on the CPU by
+# tests/golden/make_fullsize.py, which regenerates every block's plaintext and seals it with the
+# oracle (oracle/xsalsa_simd.c), so a GPU run is held to numbers the GPU never produced.
+FULLSIZE_PINS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                             "fullsize.json")
+
+
+def fullsize_pins() -> dict:
+    with open(FULLSIZE_PINS) as f:
+        return json.load(f)
+
+
+def _config3_digest() -> str:
+    c3 = fullsize_pins()["config3"]
+    if (c3["blocks"], c3["seed"], c3["key"], c3["nonce0"]) != (CONFIG3_BLOCKS, CONFIG3_SEED, CONFIG3_KEY.hex(),
+                                                                CONFIG3_NONCE0.hex()):
+        raise RuntimeError("tests/golden/fullsize.json pins another configs[3] set: rerun make_fullsize.py")
+    return c3["tag_digest"]
+
+
+# the order-independent tag digest of one pass over that set (hi || lo, hex): the CPU oracle's,
+# the same for any world size (tests/test_objectset_gpu.py, bench.py's objectset leg)
+CONFIG3_TAG_DIGEST = _config3_digest()
 
 
 def _descriptors(nonce0: bytes, gidx: np.ndarray, round_blocks: int, open_mode: bool) -> np.ndarray:

@@ -27,6 +27,13 @@ def sodium_vectors():
         return json.load(f)
 
 
+@pytest.fixture(scope="session")
+def fullsize():
+    """The CPU oracle's pins of the full-size workloads (tests/golden/make_fullsize.py)."""
+    with open(os.path.join(GOLDEN, "fullsize.json")) as f:
+        return json.load(f)
+
+
 def pytest_terminal_summary(terminalreporter, exitstatus, config):
     """Name the native library the run loaded (its build id = sha256 of the sources it was built
     from, rclone_amd/build.py), last in the output so a log's tail carries it."""

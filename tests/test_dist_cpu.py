@@ -151,3 +151,36 @@ def test_bench_rank_failure_fails_the_job():
     r, lines = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"])
     assert r.returncode != 0 and not lines
     assert "need 2 GPUs" in r.stderr or "exited with status" in r.stderr
+
+
+def test_bench_wrong_shard_fails_the_job():
+    """A rank whose shard digest is wrong (forced) makes the summed digest miss on every rank: the
+    line still prints with objectset.ok false, and the job ends non-zero."""
+    r, lines = _bench(["--gpus", "2", "--dry-run", "--steps", "1"],
+                      {"BENCH_DIST_BACKEND": "gloo", "BENCH_FORCE_DIGEST_MISMATCH": "1"})
+    assert r.returncode != 0, r.stderr[-3000:]
+    assert len(lines) == 1 and lines[0]["objectset"]["ok"] is False
+    assert "objectset leg failed" in r.stderr
+    r, lines = _bench(["--gpus", "2", "--dry-run", "--steps", "1"], {"BENCH_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0 and lines[0]["objectset"]["ok"] is True
+
+
+def test_fail_if_wrong_paths():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod2", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    bench.fail_if_wrong(True, "a", "a", 0, None)
+    bench.fail_if_wrong(True, "a", "a", 0, True)
+    for args, msg in (((False, "a", "b", 0, True), "headline tag digest a != oracle b"),
+                      ((True, "a", "a", 3, True), "3 tag failures"),
+                      ((True, "a", "a", 0, False), "objectset leg failed")):
+        with pytest.raises(SystemExit, match=msg):
+            bench.fail_if_wrong(*args)
+    # the headline pins: worlds 1/2/4/8 at 100000 blocks per rank, nothing for other layouts
+    assert len(bench.headline_expected_digest(1, 100_000, False)) == 32
+    assert bench.headline_expected_digest(8, 100_000, False) != bench.headline_expected_digest(1, 100_000, False)
+    assert bench.headline_expected_digest(3, 100_000, False) is None
+    assert bench.headline_expected_digest(1, 50_000, False) is None
+    assert bench.headline_expected_digest(1, 100_000, True) is None

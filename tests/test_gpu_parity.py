@@ -122,14 +122,32 @@ def test_tag_fail_injection(dev):
             assert out[seg] == plain[seg]
 
 
-def test_full_size_round_trip(dev):
-    # config 2 size: 100k x 64 KiB device-resident; size-independent properties + sampled oracle
-    nb = 100_000
-    key = splitmix64_bytes(41, 32)
-    n0 = splitmix64_bytes(42, 24)
+def device_sha256(t, chunk=1 << 28):
+    """SHA-256 of a device tensor's bytes, streamed to the host in 256 MiB pieces."""
+    h = hashlib.sha256()
+    flat = t.view(-1)
+    for lo in range(0, flat.numel(), chunk):
+        h.update(flat[lo:lo + chunk].cpu().numpy().data)
+    return h.hexdigest()
+
+
+def test_full_size_round_trip(dev, fullsize):
+    # configs[1] size: 100k x 64 KiB device-resident.  The whole wire body must hash to the CPU
+    # oracle's SHA-256 of the same 100k blocks (tests/golden/make_fullsize.py: every block
+    # regenerated and sealed on the CPU), plus round trip and sampled blocks against the oracle
+    p = fullsize["config1_object"]
+    nb = p["blocks"]
+    key = bytes.fromhex(p["key"])
+    n0 = bytes.fromhex(p["nonce0"])
+    assert (key, n0, nb) == (splitmix64_bytes(41, 32), splitmix64_bytes(42, 24), 100_000)
     plain = torch.empty(nb * 65536, dtype=torch.uint8, device="cuda")
-    dev.fill_random(plain, 0x5EED)
+    dev.fill_random(plain, p["seed"])
     body = dev.seal_object(key, n0, plain)
+    torch.cuda.synchronize()
+    assert device_sha256(body) == p["wire_sha256"]
+    from rclone_amd.objectset import tag_digest
+    d0, d1 = [int(x) & (2**64 - 1) for x in tag_digest(body, nb).tolist()]
+    assert f"{d1:016x}{d0:016x}" == p["tag_digest"]
     out, ok = dev.open_object(key, n0, body)
     assert bool(torch.equal(out, plain))
     assert int(ok.sum()) == nb
@@ -137,31 +155,36 @@ def test_full_size_round_trip(dev):
     host_plain = plain.view(nb, 65536)
     host_body = body.view(nb, 65552)
     for b in [0, 1, 777, 65535, 65536, nb - 1]:
-        p = host_plain[b].cpu().numpy().tobytes()
-        want = orc.seal(p, orc.nonce_add(n0, b), key)
+        pb = host_plain[b].cpu().numpy().tobytes()
+        want = orc.seal(pb, orc.nonce_add(n0, b), key)
         assert host_body[b].cpu().numpy().tobytes() == want, b
     # the device generator matches the host SplitMix64 generator
-    assert host_plain[0, :4096].cpu().numpy().tobytes() == splitmix64_bytes(0x5EED, 4096)
+    assert host_plain[0, :4096].cpu().numpy().tobytes() == splitmix64_bytes(p["seed"], 4096)
 
 
-def test_full_size_independent_objects(dev):
+def test_full_size_independent_objects(dev, fullsize):
     # config 2's other form: 100k one-block objects, each with its own random
-    # nonce (every 97th about to carry out of byte 7), through descriptor mode; every tag
-    # verified, tampered objects flagged and zero-filled, sampled objects against the oracle
+    # nonce (every 97th about to carry out of byte 7), through descriptor mode; the whole wire
+    # body against the CPU oracle's SHA-256 (tests/golden/make_fullsize.py), every tag verified,
+    # tampered objects flagged and zero-filled, sampled objects against the oracle
     from rclone_amd import shard
-    nb = 100_000
-    key = splitmix64_bytes(51, 32)
-    nonces = np.frombuffer(splitmix64_bytes(52, nb * 24), dtype=np.uint8).reshape(nb, 24).copy()
-    nonces[::97, :8] = 0xFF
+    p = fullsize["config1_independent"]
+    nb = p["blocks"]
+    key = bytes.fromhex(p["key"])
+    assert (key, nb, p["nonce_seed"], p["carry_every"]) == (splitmix64_bytes(51, 32), 100_000, 52, 97)
+    nonces = np.frombuffer(splitmix64_bytes(p["nonce_seed"], nb * 24), dtype=np.uint8).reshape(nb, 24).copy()
+    nonces[::p["carry_every"], :8] = 0xFF
     d = np.zeros(nb, dtype=shard.DESC_DTYPE)
     i = np.arange(nb, dtype=np.uint64)
     d["src"], d["dst"], d["len"], d["nonce"] = i * 65536, i * 65552, 65536, nonces
     dopen = d.copy()
     dopen["src"], dopen["dst"] = i * 65552, i * 65536
     plain = torch.empty(nb * 65536, dtype=torch.uint8, device="cuda")
-    dev.fill_random(plain, 0x0B1EC7)
+    dev.fill_random(plain, p["seed"])
     body = torch.empty(nb * 65552, dtype=torch.uint8, device="cuda")
     dev.seal_batch(key, d, plain, body)
+    torch.cuda.synchronize()
+    assert device_sha256(body) == p["wire_sha256"]
     bad = [3, 97 * 5, nb // 2 + 1, nb - 1]
     tampered = body.clone().view(nb, 65552)
     for k, b in enumerate(bad):
