@@ -179,6 +179,29 @@ def lib():
     return _lib
 
 
+_hooks = None
+
+
+def hooks_lib():
+    """TEST ONLY: the failure-injection twin of the library (build.HOOKS_LIB, xs_api.cpp under
+    -DXS_TEST_HOOKS), with the same entry points plus xs_test_fail_batch / xs_test_failed_requests.
+    Load it in a process of its own (tests/test_engine_failure_gpu.py), never beside lib()."""
+    global _hooks
+    if _hooks is None:
+        lib()  # builds both when stale
+        why = _build.stale_reason(_build.HOOKS_LIB)
+        if why is not None:
+            raise StaleLibraryError(f"{_build.HOOKS_LIB}: {why}")
+        L = ctypes.CDLL(_build.HOOKS_LIB)
+        for name, res, args in _SIGS + [("xs_test_fail_batch", None, [ctypes.c_int]),
+                                        ("xs_test_failed_requests", ctypes.c_int, [])]:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _hooks = L
+    return _hooks
+
+
 def build_id():
     return lib().xs_build_id().decode()
 

@@ -25,6 +25,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "librclone_crypt.so")
+# TEST-ONLY twin of LIB: the same objects with csrc/xs_api.cpp compiled under -DXS_TEST_HOOKS (failure
+# injection into the engine's combined batches, tests/test_engine_failure_gpu.py).  Nothing in the
+# product loads it; rclone_amd/_lib.py hooks_lib() is its only loader.
+HOOKS_LIB = os.path.join(HERE, "librclone_crypt_testhooks.so")
+HOOKS_SOURCE = "xs_api.cpp"
 HEADER = os.path.join(ROOT, "include", "rclone_crypt_gpu.h")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RCLONE_AMD_ARCH", "gfx950")
@@ -111,10 +116,19 @@ def compiler_id():
         if os.path.exists(clang):
             h.update(clang.encode() + b"\0" + str(os.path.getsize(clang)).encode() + b"\0")
         info = os.path.join(rocm, ".info")
-        if os.path.isdir(info):
-            for f in sorted(os.listdir(info)):
-                with open(os.path.join(info, f), "rb") as fh:
+        try:
+            entries = sorted(os.listdir(info)) if os.path.isdir(info) else []
+        except OSError:
+            entries = []
+        for f in entries:  # regular, readable files only: anything else never blocks a load
+            p = os.path.join(info, f)
+            try:
+                if not os.path.isfile(p):
+                    continue
+                with open(p, "rb") as fh:
                     h.update(f.encode() + b"\0" + fh.read() + b"\0")
+            except OSError:
+                continue
         _compiler_id = h.hexdigest()[:16]
     return _compiler_id
 
@@ -143,7 +157,7 @@ def stale_reason(path=LIB):
 
 
 def needs_build():
-    return stale_reason(LIB) is not None
+    return stale_reason(LIB) is not None or stale_reason(HOOKS_LIB) is not None
 
 
 def build(force=False, verbose=False):
@@ -157,31 +171,40 @@ def build(force=False, verbose=False):
         bid = build_sources_sha256()
         cc = compiler_id() or "unstamped"
         tmp = f"{LIB}.tmp{os.getpid()}"
+        tmp_hooks = f"{HOOKS_LIB}.tmp{os.getpid()}"
         # one object per source, compiled in parallel (xs_kernels.hip alone is most of the time),
         # then one link
         import tempfile
         from concurrent.futures import ThreadPoolExecutor
         with tempfile.TemporaryDirectory(prefix="rclone_amd_build_") as od:
-            def compile_one(src):
-                obj = os.path.join(od, os.path.basename(src) + ".o")
+            def compile_one(src, hooks=False):
+                obj = os.path.join(od, os.path.basename(src) + (".hooks.o" if hooks else ".o"))
                 cmd = ([HIPCC, f"--offload-arch={ARCH}"] + [f for f in FLAGS if f != "-shared"] +
-                       [f'-DXS_BUILD_ID="{bid}"', f'-DXS_BUILD_COMPILER="{cc}"', "-c", "-o", obj, src])
+                       [f'-DXS_BUILD_ID="{bid}"', f'-DXS_BUILD_COMPILER="{cc}"'] + (["-DXS_TEST_HOOKS"] if hooks else []) +
+                       ["-c", "-o", obj, src])
                 if verbose:
                     print(" ".join(cmd), file=sys.stderr)
                 subprocess.check_call(cmd)
                 return obj
             jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
+            srcs = sources()
+            hooks_src = os.path.join(CSRC, HOOKS_SOURCE)
             with ThreadPoolExecutor(jobs) as ex:
-                objs = list(ex.map(compile_one, sources()))
-            cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lpthread"]
-            if verbose:
-                print(" ".join(cmd), file=sys.stderr)
+                hooks_fut = ex.submit(compile_one, hooks_src, True)
+                objs = list(ex.map(compile_one, srcs))
+                hooks_obj = hooks_fut.result()
+            hooks_objs = [hooks_obj if src == hooks_src else o for src, o in zip(srcs, objs)]
             try:
-                subprocess.check_call(cmd)
-                os.replace(tmp, LIB)
+                for out, tmpf, ob in ((HOOKS_LIB, tmp_hooks, hooks_objs), (LIB, tmp, objs)):
+                    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmpf] + ob + ["-lpthread"]
+                    if verbose:
+                        print(" ".join(cmd), file=sys.stderr)
+                    subprocess.check_call(cmd)
+                    os.replace(tmpf, out)
             finally:
-                if os.path.exists(tmp):
-                    os.unlink(tmp)
+                for tmpf in (tmp, tmp_hooks):
+                    if os.path.exists(tmpf):
+                        os.unlink(tmpf)
     return LIB
 
 

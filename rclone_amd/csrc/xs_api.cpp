@@ -120,8 +120,10 @@ const char* xs_version(void) { return "rclone_amd crypt 0.1 (gfx950)"; }
 #endif
 __attribute__((used)) static const char kBuildIdTag[] = "xs-build-id:" XS_BUILD_ID;
 const char* xs_build_id(void) { return kBuildIdTag + 12; }
-// the compiler that built it (sha256 of `hipcc --version`, first 16 hex digits): the loader rebuilds a
-// library whose compiler differs from the one installed next to the tree
+// the compiler that built it (rclone_amd/build.py compiler_id: the first 16 hex digits of a sha256
+// over the resolved hipcc and clang paths, the clang binary's size and the ROCm .info release
+// files -- file-system facts, hipcc is never run): the loader rebuilds a library whose compiler
+// differs from the one installed next to the tree
 #ifndef XS_BUILD_COMPILER
 #define XS_BUILD_COMPILER "unstamped"
 #endif
@@ -896,11 +898,31 @@ static int engine_issue_zero_copy(xs_engine::CSlot& c, const std::vector<uint64_
   return XS_OK;
 }
 
+#ifdef XS_TEST_HOOKS
+// TEST-ONLY failure injection (compiled into librclone_crypt_testhooks.so alone, rclone_amd/build.py):
+// the first combined batch of at least g_fail_min requests issued after xs_test_fail_batch(min)
+// fails before any launch, as a HIP error would; every request it carried must get XS_ERR_HIP.
+static std::atomic<int> g_fail_min{0}, g_failed_reqs{0};
+extern "C" void xs_test_fail_batch(int min_reqs) {
+  g_failed_reqs = 0;
+  g_fail_min = min_reqs;
+}
+extern "C" int xs_test_failed_requests(void) { return g_failed_reqs.load(); }
+#endif
+
 // Issue one combined batch on coalescing slot c (asynchronously).  The slot's stream carries only
 // this batch, so the stream's completion is the batch's: no event is recorded (one runtime call
 // less per batch; concurrent callers' launches serialise inside the runtime).
 static int engine_issue_batch(xs_engine* e, xs_engine::CSlot& c) {
   auto& batch = c.batch;
+#ifdef XS_TEST_HOOKS
+  int want = g_fail_min.load();
+  if (want > 0 && (int)batch.size() >= want && g_fail_min.compare_exchange_strong(want, 0)) {
+    g_failed_reqs = (int)batch.size();
+    set_error("test hook: injected failure of a combined batch of %zu requests", batch.size());
+    return XS_ERR_HIP;
+  }
+#endif
   c.spin = false;  // only a fused zero-copy launch sets it
   if (hipSetDevice(e->device) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
   // seal requests first, then open; inside a direction, requests with equal keys adjacent

@@ -14,6 +14,7 @@
 #include <sys/syscall.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cctype>
 #include <cstdio>
 #include <cstdlib>
@@ -109,14 +110,57 @@ int parse_device_list(const char* s, std::vector<int>* out) {
   return (int)out->size();
 }
 
-// The process's CPU affinity: the main thread's mask (what the operator gave the process with
-// taskset / numactl / the container, and what `taskset -p` or a cpuset change moves later), read
-// again whenever the library sizes a pool or pins one of its threads -- so a mask narrowed or
-// widened after load is honoured.  Read by pid, not by the calling thread, so a thread the
-// library has already pinned to one node does not shrink it.  The mask at load is the fallback
-// when the main thread cannot be queried.
+// The process's cgroup v2 path ("/a/b" from "0::/a/b" in /proc/self/cgroup; "" when unknown)
+static std::string self_cgroup() {
+  const char* proc = getenv("RCLONE_AMD_PROC_ROOT");
+  std::string self;
+  FILE* f = fopen(((proc && *proc ? std::string(proc) : std::string("/proc")) + "/self/cgroup").c_str(), "r");
+  if (f) {
+    char buf[4096];
+    while (fgets(buf, sizeof buf, f)) {
+      if (strncmp(buf, "0::", 3) == 0) {
+        self.assign(buf + 3);
+        while (!self.empty() && isspace((unsigned char)self.back())) self.pop_back();
+        break;
+      }
+    }
+    fclose(f);
+  }
+  if (self == "/" || self.find("..") != std::string::npos) self.clear();
+  return self;
+}
+
+// The CPUs the process's cgroup allows (cgroup v2 cpuset.cpus.effective of its own group, else of
+// the mount root); false when no such file is readable.  This is what `docker --cpuset-cpus`, a
+// systemd AllowedCPUs= or a cpuset update after load set for the whole process.
+static bool cgroup_cpuset(cpu_set_t* set) {
+  const std::string base = sysfs_root() + "/fs/cgroup";
+  std::string v;
+  const std::string self = self_cgroup();
+  if (!(!self.empty() && read_line(base + self + "/cpuset.cpus.effective", &v)) &&
+      !read_line(base + "/cpuset.cpus.effective", &v))
+    return false;
+  std::vector<int> cpus;
+  if (!parse_cpulist(v.c_str(), &cpus) || cpus.empty()) return false;
+  CPU_ZERO(set);
+  for (int c : cpus)
+    if (c < CPU_SETSIZE) CPU_SET(c, set);
+  return CPU_COUNT(set) > 0;
+}
+
+// The process's CPU affinity, read again whenever the library sizes a pool or pins one of its
+// threads.  Its first source is the main thread's mask (read by pid, not by the calling thread, so
+// a thread the library has already pinned to one node does not shrink it): what the operator gave
+// the process with taskset / numactl / the container.  That mask can also be narrowed by the host
+// program itself -- OMP_PROC_BIND binding the initial thread, an embedding runtime pinning its main
+// thread -- which says nothing about the CPUs the process may use.  So when it is
+// narrower than the mask captured at load, the union of the two counts, cut to the cgroup's cpuset
+// when one is readable (a cpuset narrowed after load is the operator's, and is honoured), and the
+// library says so once on stderr.  The mask at load is the fallback when the main thread cannot be
+// queried.
 static cpu_set_t g_process_cpus;
 static bool g_process_cpus_ok = false;
+static std::atomic<bool> g_narrow_logged{false};
 
 void capture_process_affinity() {
   CPU_ZERO(&g_process_cpus);
@@ -127,9 +171,29 @@ void capture_process_affinity() {
 
 static bool process_cpus(cpu_set_t* set) {
   CPU_ZERO(set);
-  if (sched_getaffinity(getpid(), sizeof *set, set) == 0 && CPU_COUNT(set) > 0) return true;
-  if (!g_process_cpus_ok) return false;
-  *set = g_process_cpus;
+  cpu_set_t cur;
+  CPU_ZERO(&cur);
+  if (!(sched_getaffinity(getpid(), sizeof cur, &cur) == 0 && CPU_COUNT(&cur) > 0)) {
+    if (!g_process_cpus_ok) return false;
+    *set = g_process_cpus;
+    return true;
+  }
+  *set = cur;
+  if (!g_process_cpus_ok || CPU_COUNT(&cur) >= CPU_COUNT(&g_process_cpus)) return true;
+  cpu_set_t u, cs;
+  CPU_OR(&u, &cur, &g_process_cpus);
+  if (cgroup_cpuset(&cs)) {
+    cpu_set_t in;
+    CPU_AND(&in, &u, &cs);
+    if (CPU_COUNT(&in) > 0) u = in;
+  }
+  *set = u;
+  if (!g_narrow_logged.exchange(true))
+    fprintf(stderr,
+            "rclone_amd: the main thread's CPU mask (%d CPUs) is narrower than the process's at load (%d); "
+            "pool sizing and thread pinning use %d CPUs (load-time mask%s)\n",
+            CPU_COUNT(&cur), CPU_COUNT(&g_process_cpus), CPU_COUNT(&u),
+            CPU_COUNT(&u) < CPU_COUNT(&g_process_cpus) ? " cut to the cgroup cpuset" : "");
   return true;
 }
 
@@ -148,20 +212,7 @@ static double cgroup_v2_quota(const std::string& root) {
     }
     return true;
   };
-  const char* proc = getenv("RCLONE_AMD_PROC_ROOT");
-  std::string self;
-  FILE* f = fopen(((proc && *proc ? std::string(proc) : std::string("/proc")) + "/self/cgroup").c_str(), "r");
-  if (f) {
-    char buf[4096];
-    while (fgets(buf, sizeof buf, f)) {
-      if (strncmp(buf, "0::", 3) == 0) {
-        self.assign(buf + 3);
-        while (!self.empty() && isspace((unsigned char)self.back())) self.pop_back();
-        break;
-      }
-    }
-    fclose(f);
-  }
+  std::string self = self_cgroup();
   const std::string base = root + "/fs/cgroup";
   // walk /a/b -> /a -> "" (the mount root); a path that does not resolve under this mount (a
   // cgroup namespace shows "/") simply finds no files below the root

@@ -40,6 +40,10 @@
 extern "C" {
 void orc_encrypt_file(uint8_t* out, const uint8_t* in, int64_t len, const uint8_t nonce0[24], const uint8_t key[32]);
 void orc_nonce_add(uint8_t n[24], uint64_t x);
+// stub_engine.cpp's failure injection
+long stub_engine_submissions(void);
+long stub_engine_failed(void);
+void stub_engine_fail(long from, long count);
 }
 
 static int g_fail = 0;
@@ -754,27 +758,44 @@ static void test_topology() {
     });
     t3.join();
     const int counted = xs::effective_cpus();
-    // the mask changes after load (taskset -p / a cpuset update), with no capture call: the next
-    // pool sizing and pinning follow it
+    // the main thread's mask narrows after load, with no capture call (OMP_PROC_BIND binding the
+    // host program's initial thread, or taskset -p on its pid): the load-time mask still counts,
+    // so pool sizing does not drop to one CPU and pinning still finds the node's CPUs
     cpu_set_t one;
     CPU_ZERO(&one);
     CPU_SET(2, &one);
     sched_setaffinity(0, sizeof one, &one);
     const int counted_one = xs::effective_cpus();
-    int moved_ok = 0;
+    int kept_ok = 0;
     std::thread t4([&] {
-      xs::pin_thread_to_node(3);  // node {0,1} & mask {2} = {}: left on the process mask
+      xs::pin_thread_to_node(3);  // node {0,1} & (mask {2} | load {1,2}) = {1}
+      cpu_set_t s;
+      CPU_ZERO(&s);
+      if (sched_getaffinity(0, sizeof s, &s) == 0) kept_ok = CPU_COUNT(&s) == 1 && CPU_ISSET(1, &s);
+    });
+    t4.join();
+    // ... but a cgroup cpuset narrowed to {2} after load is the operator's: honoured
+    put_file(r + "/fs/cgroup/cpuset.cpus.effective", "2\n");
+    const int counted_cpuset = xs::effective_cpus();
+    int moved_ok = 0;
+    std::thread t5([&] {
+      xs::pin_thread_to_node(3);  // node {0,1} & {2} = {}: left on the process mask
       cpu_set_t s;
       CPU_ZERO(&s);
       if (sched_getaffinity(0, sizeof s, &s) == 0) moved_ok = CPU_COUNT(&s) == 1 && CPU_ISSET(2, &s);
     });
-    t4.join();
+    t5.join();
+    remove((r + "/fs/cgroup/cpuset.cpus.effective").c_str());
     sched_setaffinity(0, sizeof full, &full);
     const int counted_full = xs::effective_cpus();
     xs::capture_process_affinity();
-    CHECK(counted_one == 1 || getenv("RCLONE_AMD_CPUS"), "effective_cpus follows a mask narrowed after load (%d)", counted_one);
+    CHECK(counted_one == 2 || getenv("RCLONE_AMD_CPUS"), "a main thread narrowed after load keeps the load mask (%d)",
+          counted_one);
+    CHECK(kept_ok, "pinning uses the load-time mask while only the main thread is narrowed");
+    CHECK(counted_cpuset == 1 || getenv("RCLONE_AMD_CPUS"), "effective_cpus follows a cpuset narrowed after load (%d)",
+          counted_cpuset);
     CHECK(counted_full >= counted || getenv("RCLONE_AMD_CPUS"), "effective_cpus follows a mask widened again (%d)", counted_full);
-    CHECK(moved_ok, "library threads stay inside the mask as it is now");
+    CHECK(moved_ok, "library threads stay inside the cgroup cpuset as it is now");
     CHECK(inter_ok, "pinning intersects the node with the process mask");
     CHECK(disjoint_ok, "no pinning outside the process mask when the node is disjoint from it");
     CHECK(counted == 2 || getenv("RCLONE_AMD_CPUS"), "effective_cpus counts the process mask (%d)", counted);
@@ -833,6 +854,161 @@ static void test_md5_tiers() {
   for (auto& x : th) x.join();
   CHECK(bad == 0, "%d streams hashed wrongly through the tiers", bad.load());
   CHECK(!xs::md5_x16_supported() || xs::md5_tier_stats().lanes.load() > lanes0, "engine lanes used");
+}
+
+// ---------------------------------------------------------------- a failing GPU engine
+// A GPU submission that fails (stub_engine_fail: XS_ERR_HIP, as a HIP error in xs_api.cpp would be)
+// must surface as RC_ERR_GPU at the refill that made it, exactly as the reference surfaces any
+// error there: no byte of the failed batch is served, the error is sticky through later Reads and
+// RangeSeek (encrypter/decrypter finish, cipher.go:748-758, :1042-1052), Close still closes the
+// source once and then reports ErrorFileClosed (:1069-1087), and other handles on the same cipher
+// keep working.  Refills ramp 1, 2, 4, 8, 8, ... blocks (growth 2, batch 8), so failing refill k
+// leaves exactly the first 2^k - 1 blocks served.
+static void test_engine_failure(rc_cipher* c, const uint8_t key[32]) {
+  const std::vector<uint8_t> plain = rbytes(40 * 65536 + 123);
+  const std::vector<uint8_t> nonce = rbytes(24);
+  const std::vector<uint8_t> want = oracle_file(plain, nonce.data(), key);
+  rc_cipher_set_batch_blocks(c, 8);
+  rc_cipher_set_readahead_growth(c, 2);
+  const long failed0 = stub_engine_failed();
+  for (int k = 0; k < 5; k++) {
+    const size_t blocks_before = k < 4 ? (1u << k) - 1 : 15;  // refills 1, 2, 4, 8 then 8
+    const size_t wire_before = 32 + blocks_before * 65552, plain_before = blocks_before * 65536;
+    // encrypter
+    Src s;
+    s.p = plain.data();
+    s.n = plain.size();
+    int32_t err = 0;
+    rc_encrypter* e = rc_encrypt_data(c, mk(&s), nonce.data(), &err);
+    stub_engine_fail(stub_engine_submissions() + k, 1);
+    std::vector<uint8_t> ct;
+    err = drain_enc(e, ct);
+    stub_engine_fail(-1, 0);
+    CHECK(err == RC_ERR_GPU, "encrypter: refill %d failed with %d", k, err);
+    CHECK(ct.size() == wire_before && std::equal(ct.begin(), ct.end(), want.begin()),
+          "encrypter: refill %d failed after %zu bytes (want the %zu before it)", k, ct.size(), wire_before);
+    uint8_t b[64];
+    CHECK(rc_encrypter_read(e, b, 64, &err) == 0 && err == RC_ERR_GPU, "encrypter: sticky error %d", err);
+    CHECK(rc_encrypter_read(e, b, 1, &err) == 0 && err == RC_ERR_GPU, "encrypter: sticky error again %d", err);
+    // another handle on the same cipher while this one is failed: unaffected
+    {
+      Src s2;
+      s2.p = plain.data();
+      s2.n = 3 * 65536 + 5;
+      rc_encrypter* e2 = rc_encrypt_data(c, mk(&s2), nonce.data(), &err);
+      std::vector<uint8_t> ct2;
+      std::vector<uint8_t> p2(plain.begin(), plain.begin() + (long)s2.n);
+      CHECK(drain_enc(e2, ct2) == RC_EOF && ct2 == oracle_file(p2, nonce.data(), key), "other encrypter");
+      rc_encrypter_free(e2);
+    }
+    rc_encrypter_free(e);
+    // decrypter (DecryptData): the header read makes no submission
+    Src d;
+    d.p = want.data();
+    d.n = want.size();
+    rc_decrypter* h = rc_decrypt_data(c, mk(&d), &err);
+    CHECK(h && err == RC_NIL, "decrypt_data %d", err);
+    if (!h) continue;
+    stub_engine_fail(stub_engine_submissions() + k, 1);
+    std::vector<uint8_t> pt;
+    err = drain_dec(h, pt);
+    stub_engine_fail(-1, 0);
+    CHECK(err == RC_ERR_GPU, "decrypter: refill %d failed with %d", k, err);
+    CHECK(pt.size() == plain_before && std::equal(pt.begin(), pt.end(), plain.begin()),
+          "decrypter: refill %d failed after %zu bytes (want the %zu before it)", k, pt.size(), plain_before);
+    CHECK(rc_decrypter_read(h, b, 64, &err) == 0 && err == RC_ERR_GPU, "decrypter: sticky error %d", err);
+    rc_decrypter_range_seek(h, 0, 0, -1, &err);  // not opened with a seek callback: finish() returns the set error
+    CHECK(err == RC_ERR_GPU, "decrypter: RangeSeek after the failure returned %d", err);
+    CHECK(rc_decrypter_close(h) == RC_NIL && d.closes == 1, "decrypter close after the failure");
+    CHECK(rc_decrypter_read(h, b, 64, &err) == 0 && err == RC_ERR_FILE_CLOSED, "read after close %d", err);
+    CHECK(rc_decrypter_close(h) == RC_ERR_FILE_CLOSED && d.closes == 1, "second close");
+    rc_decrypter_free(h);
+  }
+  // DecryptDataSeek: its RangeSeek fills the first block itself (cipher.go:1027-1031), so a failure
+  // there fails the open -- no handle, RC_ERR_GPU, every source it opened closed
+  // (newDecrypterSeek, :826-832); a failure at the next refill serves the rest of the first block,
+  // then RC_ERR_GPU, and a RangeSeek after it returns that sticky error (finished with an error
+  // other than EOF, :976-980)
+  for (int at = 0; at < 2; at++) {
+    OpenCtx o{&want, {}, {}};
+    int32_t err = 0;
+    stub_engine_fail(stub_engine_submissions() + at, 1);
+    rc_decrypter* h = rc_decrypt_data_seek(c, open_cb, &o, 70000, -1, &err);
+    if (at == 0) {
+      stub_engine_fail(-1, 0);
+      CHECK(!h && err == RC_ERR_GPU, "seek open with a failed first fill: %d", err);
+      bool closed = !o.srcs.empty();
+      for (auto* x : o.srcs) closed = closed && x->closes == 1;
+      CHECK(closed, "seek open: sources closed after the failure");
+    } else {
+      CHECK(h && err == RC_NIL, "decrypt_data_seek %d", err);
+      if (h) {
+        std::vector<uint8_t> pt;
+        err = drain_dec(h, pt);
+        stub_engine_fail(-1, 0);
+        CHECK(err == RC_ERR_GPU && pt.size() == 131072 - 70000 &&
+                  std::equal(pt.begin(), pt.end(), plain.begin() + 70000),
+              "seek decrypter: %d after %zu bytes", err, pt.size());
+        rc_decrypter_range_seek(h, 0, 0, -1, &err);
+        CHECK(err == RC_ERR_GPU, "seek decrypter RangeSeek %d", err);
+        CHECK(rc_decrypter_close(h) == RC_NIL, "seek decrypter close");
+        rc_decrypter_free(h);
+      }
+    }
+    stub_engine_fail(-1, 0);
+    for (auto* x : o.srcs) delete x;
+  }
+  // computeHashWithNonce: the failed seal is the call's error, no digest; the next call succeeds
+  {
+    Src s;
+    s.p = plain.data();
+    s.n = plain.size();
+    uint8_t md5[16] = {0}, zero[16] = {0};
+    stub_engine_fail(stub_engine_submissions() + 2, 1);
+    const int32_t e1 = rc_compute_hash_with_nonce(c, mk(&s), nonce.data(), md5);
+    stub_engine_fail(-1, 0);
+    CHECK(e1 == RC_ERR_GPU && !memcmp(md5, zero, 16) && s.closes == 1, "hash with a failed seal: %d", e1);
+    Src s2;
+    s2.p = plain.data();
+    s2.n = plain.size();
+    CHECK(rc_compute_hash_with_nonce(c, mk(&s2), nonce.data(), md5) == RC_NIL &&
+              std::vector<uint8_t>(md5, md5 + 16) == md5_of(want.data(), want.size()),
+          "hash after the failure");
+  }
+  // concurrent streams (TSan): 8 writers of 20 blocks, 5 refills each; three consecutive
+  // submissions fail, so exactly three streams end with RC_ERR_GPU after a correct prefix and
+  // the other five complete bit-exact
+  {
+    std::atomic<int> failed{0}, bad{0};
+    std::vector<std::vector<uint8_t>> outs(8);
+    const long base = stub_engine_submissions();
+    stub_engine_fail(base + 10, 3);
+    std::vector<std::thread> th;
+    for (int t = 0; t < 8; t++)
+      th.emplace_back([&, t] {
+        Src s;
+        s.p = plain.data();
+        s.n = 20 * 65536;
+        int32_t err = 0;
+        rc_encrypter* e = rc_encrypt_data(c, mk(&s), nonce.data(), &err);
+        std::vector<uint8_t> ct;
+        err = drain_enc(e, ct);
+        const size_t full = 32 + 20 * 65552;
+        if (err == RC_ERR_GPU) {
+          failed++;
+          if (ct.size() >= full || !std::equal(ct.begin(), ct.end(), want.begin())) bad++;
+        } else if (err != RC_EOF || ct.size() != full || !std::equal(ct.begin(), ct.end(), want.begin())) {
+          bad++;
+        }
+        rc_encrypter_free(e);
+      });
+    for (auto& x : th) x.join();
+    stub_engine_fail(-1, 0);
+    CHECK(failed == 3 && bad == 0, "concurrent: %d streams failed (want 3), %d bad", failed.load(), bad.load());
+  }
+  CHECK(stub_engine_failed() - failed0 == 5 * 2 + 2 + 1 + 3, "injected failures %ld", stub_engine_failed() - failed0);
+  rc_cipher_set_batch_blocks(c, 64);
+  rc_cipher_set_readahead_growth(c, 0);
 }
 
 // ---------------------------------------------------------------- concurrency (TSan)
@@ -925,6 +1101,7 @@ int main(int argc, char** argv) {
   rc_cipher_keys(c, key, nullptr, nullptr);
   if (only_concurrency) {
     test_concurrency(c, key);
+    test_engine_failure(c, key);
     test_md5_tiers();
   } else {
     test_md5_tiers();
@@ -937,6 +1114,7 @@ int main(int argc, char** argv) {
     test_topology();
     test_encrypter_md5(c, key);
     test_seek_grid(c, key);
+    test_engine_failure(c, key);
     test_names(c);
   }
   rc_cipher_free(c);

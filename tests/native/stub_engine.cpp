@@ -7,6 +7,7 @@
 // implemented here with the CPU oracle (oracle/xsalsa_oracle.c, oracle/eme_oracle.c), which is the
 // checker the rest of the test suite uses; the device contract is kept: failed blocks are
 // zero-filled with ok = 0, descriptor order and nonces as in xs_api.cpp.
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -41,6 +42,20 @@ void set_error(const char* fmt, ...) {
 std::vector<int> default_devices() { return {0}; }
 }  // namespace xs
 
+// Failure injection (tests): every engine submission (seal, open, ranged open -- one GPU batch each
+// in the real library) takes a number from one process-wide counter; submissions numbered
+// [g_fail_from, g_fail_from + g_fail_count) fail as a HIP error would (XS_ERR_HIP, last error set),
+// writing nothing.  stub_engine_fail(-1, 0) turns it off.
+static std::atomic<long> g_submits{0}, g_fail_from{-1}, g_fail_count{0}, g_failed{0};
+static bool inject_failure() {
+  const long k = g_submits.fetch_add(1);
+  const long f = g_fail_from.load();
+  if (f < 0 || k < f || k >= f + g_fail_count.load()) return false;
+  g_failed++;
+  xs::set_error("stub engine: injected failure of submission %ld", k);
+  return true;
+}
+
 struct xs_engine {
   std::mutex mu;
   uint64_t calls = 0;
@@ -53,6 +68,12 @@ struct xs_pool {
 };
 
 extern "C" {
+long stub_engine_submissions(void) { return g_submits.load(); }
+long stub_engine_failed(void) { return g_failed.load(); }
+void stub_engine_fail(long from, long count) {
+  g_fail_count = count;
+  g_fail_from = from;
+}
 const char* xs_last_error(void) { return xs::g_err.c_str(); }
 void* xs_host_alloc(size_t bytes) { return malloc(bytes ? bytes : 1); }
 void* xs_host_alloc_node(size_t bytes, int) { return malloc(bytes ? bytes : 1); }
@@ -70,6 +91,7 @@ int xs_engine_seal(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24]
                    const void* plain, uint64_t plain_len, void* body) {
   std::lock_guard<std::mutex> g(e->mu);
   e->calls++;
+  if (inject_failure()) return XS_ERR_HIP;
   const uint8_t* in = (const uint8_t*)plain;
   uint8_t* out = (uint8_t*)body;
   for (uint64_t j = 0; j * XS_BLOCK_DATA < plain_len; j++) {
@@ -86,6 +108,7 @@ int xs_engine_open(xs_engine* e, const uint8_t key[32], const uint8_t nonce0[24]
                    const void* body, uint64_t body_len, void* plain, uint8_t* ok) {
   std::lock_guard<std::mutex> g(e->mu);
   e->calls++;
+  if (inject_failure()) return XS_ERR_HIP;
   if (getenv("STUB_TRACE"))
     fprintf(stderr, "open fb=%llu len=%llu in%%16=%u out%%16=%u\n", (unsigned long long)first_block,
             (unsigned long long)body_len, (unsigned)((uintptr_t)body & 15u), (unsigned)((uintptr_t)plain & 15u));
@@ -133,7 +156,8 @@ int xs_pool_seal_md5(xs_pool*, const uint8_t key[32], uint64_t nobj, const uint8
     const uint64_t nb = (lens[i] + XS_BLOCK_DATA - 1) / XS_BLOCK_DATA;
     std::vector<uint8_t> body(lens[i] + nb * XS_BLOCK_HDR + 1);
     xs_engine e;
-    xs_engine_seal(&e, key, nonces + 24 * i, 0, (const uint8_t*)plain + offs[i], lens[i], body.data());
+    if (xs_engine_seal(&e, key, nonces + 24 * i, 0, (const uint8_t*)plain + offs[i], lens[i], body.data()) != XS_OK)
+      return XS_ERR_HIP;
     xs::HostMd5 m;
     static const uint8_t magic[8] = {'R', 'C', 'L', 'O', 'N', 'E', 0, 0};
     m.update(magic, 8);

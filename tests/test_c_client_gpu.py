@@ -127,7 +127,7 @@ def test_shim_data_path_cpu_stub_tsan(tmp_path, ref_kat, sodium_vectors):
     subprocess.check_call(["make", "-s", "-C", NATIVE, "build/c_client_stub_tsan"])
     exe = os.path.join(NATIVE, "build", "c_client_stub_tsan")
     pick = lambda files: [i for i, f in enumerate(files)  # noqa: E731
-                          if f["plain"] == "splitmix64" and f["size"] in (0, 17, 65536, 65537) or f["size"] > 196608]
+                          if f["plain"] == "splitmix64" and (f["size"] in (0, 17, 65536, 65537) or f["size"] > 196608)]
     for tag, (key, cases) in zip(("ref", "sod"), _cases(ref_kat, sodium_vectors, pick)):
         _run_group(exe, tmp_path, tag, key, cases, timeout=600, threads=4, extra_env={"TSAN_OPTIONS": "halt_on_error=1"})
 

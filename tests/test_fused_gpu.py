@@ -146,11 +146,11 @@ print(json.dumps({"bad": bad[:10], "nbad": len(bad), "cases": cases, "digest": h
 """
 
 
-def _run(fused_max):
+def _run(fused_max, **knobs):
     # the leader holds new requests while a batch is in flight and express lanes are off, so the
     # concurrent phase forms multi-request fused batches (the path this test is about)
     env = dict(os.environ, XS_FUSED_MAX=str(fused_max), XS_ENGINE_ZERO_COPY="1", XS_ENGINE_COALESCE="1",
-               XS_ENGINE_OVERLAP="0", XS_EXPRESS_MAX="0")
+               XS_ENGINE_OVERLAP="0", XS_EXPRESS_MAX="0", **{k: str(v) for k, v in knobs.items()})
     r = subprocess.run([sys.executable, "-c", SCRIPT % {"root": ROOT}], capture_output=True, text=True, timeout=240,
                        env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -161,12 +161,16 @@ def _run(fused_max):
 def test_fused_and_two_launch_paths_agree_with_oracle():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
+    # the launch path's operator knobs: the defaults, no fused kernel, the fused
+    # kernel without the host key setup (XS_KEY_PRE_MAX=0), and two launches with the one-wave
+    # crypt kernels even for the smallest batches (XS_SPLIT_MAX=0): the same bytes and verdicts
     fused, split = _run(16), _run(0)
-    for v in (fused, split):
+    nopre, nosplit = _run(16, XS_KEY_PRE_MAX=0), _run(0, XS_SPLIT_MAX=0)
+    for v in (fused, split, nopre, nosplit):
         assert v["bad"] == [], (v["nbad"], v["bad"])
     assert fused["concurrent"]["batches"] < fused["concurrent"]["requests"]  # the concurrent opens did coalesce
-    assert fused["cases"] == split["cases"] > 150
-    assert fused["digest"] == split["digest"]
+    assert fused["cases"] == split["cases"] == nopre["cases"] == nosplit["cases"] > 150
+    assert fused["digest"] == split["digest"] == nopre["digest"] == nosplit["digest"]
 
 
 def test_first_fused_open_on_fresh_engines_reports_tampering():

@@ -29,6 +29,17 @@ def test_library_exports_every_header_symbol():
     assert set(syms) <= set(_lib.SYMBOLS) | {"xs_engine_create"}
 
 
+def test_failure_hooks_only_in_the_test_library():
+    # xs_api.cpp's failure injection (-DXS_TEST_HOOKS) is compiled into the test-only twin alone:
+    # the product library has no such entry points, the twin has them and the same build id
+    import ctypes
+    from rclone_amd import build
+    assert not hasattr(_lib.lib(), "xs_test_fail_batch")
+    h = ctypes.CDLL(build.HOOKS_LIB)
+    assert hasattr(h, "xs_test_fail_batch") and hasattr(h, "xs_test_failed_requests")
+    assert build.library_build_id(build.HOOKS_LIB) == build.library_build_id(build.LIB)
+
+
 def test_version_and_devices():
     lib = _lib.lib()
     assert b"gfx950" in lib.xs_version()
@@ -114,7 +125,7 @@ if "-c" in args:
     open(out, "wb").close()
 else:
     with open({log!r}, "a") as f:
-        f.write("link %d\n" % os.getpid())
+        f.write("link %d %s\n" % (os.getpid(), os.path.basename(out).split(".so")[0]))
     shutil.copyfile({lib!r}, out)
 """
 
@@ -164,7 +175,10 @@ def test_concurrent_loaders_rebuild_once(tmp_path):
         assert p.returncode == 0, e[-2000:]
     ids = {o.split("ID", 1)[1].strip() for o, _ in outs}
     assert ids == {want}
-    assert log.read_text().count("link") == 1
+    # one build: the library and its test-only twin linked once each (a second build would link
+    # both again)
+    links = [ln.split() for ln in log.read_text().splitlines()]
+    assert sorted(x[2] for x in links) == ["librclone_crypt", "librclone_crypt_testhooks"], links
     assert build.library_build_id(str(pkg / "librclone_crypt.so")) == want
 
 
@@ -299,10 +313,10 @@ def test_reopen_error_keeps_the_openers_error():
 
 
 def test_ablation_patches_still_apply():
-    """tools/ablate_variant.py keeps the diagnostic (wrong-output) kernel variants out of the
+    """tools/archive/ablate_variant.py keeps the diagnostic (wrong-output) kernel variants out of the
     product file as text patches; their anchors must follow the product kernel or they rot."""
     import importlib.util
-    spec = importlib.util.spec_from_file_location("ablate_variant", os.path.join(ROOT, "tools", "ablate_variant.py"))
+    spec = importlib.util.spec_from_file_location("ablate_variant", os.path.join(ROOT, "tools", "archive", "ablate_variant.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     src = open(mod.SRC).read()

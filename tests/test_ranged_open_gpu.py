@@ -95,8 +95,8 @@ print(json.dumps({"bad": bad[:10], "nbad": len(bad), "cases": cases, "skipped_gr
 """
 
 
-def _run(fused_max):
-    env = dict(os.environ, XS_FUSED_MAX=str(fused_max), XS_ENGINE_ZERO_COPY="1")
+def _run(fused_max, knobs=None):
+    env = dict(os.environ, XS_FUSED_MAX=str(fused_max), XS_ENGINE_ZERO_COPY="1", **(knobs or {}))
     r = subprocess.run([sys.executable, "-c", SCRIPT % {"root": ROOT, "fused": 1 if fused_max else 0}],
                        capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -104,11 +104,13 @@ def _run(fused_max):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("fused_max", [16, 0])
-def test_ranged_open_matches_oracle(fused_max):
+@pytest.mark.parametrize("fused_max,knobs", [(16, None), (0, None), (16, {"XS_KEY_PRE_MAX": "0"}),
+                                             (0, {"XS_SPLIT_MAX": "0"})],
+                         ids=["fused", "two_launch", "fused_no_host_key", "two_launch_no_split"])
+def test_ranged_open_matches_oracle(fused_max, knobs):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    v = _run(fused_max)
+    v = _run(fused_max, knobs)
     assert v["bad"] == [], (v["nbad"], v["bad"])
     assert v["cases"] > 400
     if fused_max:

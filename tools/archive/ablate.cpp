@@ -1,5 +1,5 @@
 // Diagnostic: time xs_crypt<seal> / <open> over 100k resident 64 KiB blocks, linked against a kernel
-// TU (the product xs_kernels.hip, or an ablation copy made by tools/ablate_variant.py).  Not part of
+// TU (the product xs_kernels.hip, or an ablation copy made by tools/archive/ablate_variant.py).  Not part of
 // the product.
 #include <hip/hip_runtime.h>
 #include <cstdio>

@@ -1,5 +1,5 @@
 // Paired A/B timing of two builds of the crypt kernels in ONE process: build A is namespace
-// xs (xs_kernels.hip at a git revision, see tools/abtest.sh), build B is the working tree
+// xs (xs_kernels.hip at a git revision, see tools/archive/abtest.sh), build B is the working tree
 // compiled with -Dxs=xs_b plus the variant's macros.  Each build runs its own keygen.
 // Launches alternate A, B, A, B, ... over 100k resident random blocks, so clock/power drift
 // hits both; reports medians and the median of per-pair ratios B/A for keygen, seal and open,

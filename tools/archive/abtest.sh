@@ -1,10 +1,10 @@
 #!/bin/bash
 # Build tools/abtest_<name>: A = xs_kernels.hip at git revision $AREF (default HEAD) or, with
 # AREF=tree, the working tree; B = the working tree's xs_kernels.hip with the given -D macros.
-#   usage: [AREF=<rev>|tree] tools/abtest.sh <name> [-DMACRO=...]...
+#   usage: [AREF=<rev>|tree] tools/archive/abtest.sh <name> [-DMACRO=...]...
 #   AFLAGS="-D..." adds macros to build A as well.
 set -e
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 name=$1; shift
 D=/tmp/abtest
 mkdir -p $D
@@ -21,5 +21,5 @@ mkdir -p $D/include && cp include/rclone_crypt_gpu.h $D/include/
 sed -i 's#"../../include/rclone_crypt_gpu.h"#"include/rclone_crypt_gpu.h"#' $D/xs_internal.h
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c $D/a_src.hip -I $D $AFLAGS -o $D/a.o
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c rclone_amd/csrc/xs_kernels.hip -I rclone_amd/csrc -Dxs=xs_b "$@" -o $D/b_$name.o
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -c tools/abtest.cpp -I rclone_amd/csrc -o $D/t.o
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -c tools/archive/abtest.cpp -I rclone_amd/csrc -o $D/t.o
 hipcc --offload-arch=gfx950 $D/t.o $D/a.o $D/b_$name.o -o tools/abtest_$name

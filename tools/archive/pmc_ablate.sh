@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes over a tools/ablate* binary (diagnostic builds of the crypt kernels).
-# usage: tools/pmc_ablate.sh <binary> <outdir-under-gpurun_out>
+# usage: tools/archive/pmc_ablate.sh <binary> <outdir-under-gpurun_out>
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 BIN=$R/$1

@@ -1,4 +1,4 @@
-# paired A/B of kernel variants (tools/abtest.sh builds); every variant runs, failures reported
+# paired A/B of kernel variants (tools/archive/abtest.sh builds); every variant runs, failures reported
 mkdir -p gpurun_out
 rc=0
 for v in ${AB_VARIANTS:-imm mad lx1 lx2 all1 vf allvf r12 allr}; do

@@ -18,25 +18,33 @@ from pmc_summary import load  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from rclone_amd.build import KERNEL_SOURCES, kernel_sources_sha256  # noqa: E402
+from rclone_amd.build import KERNEL_SOURCES, build_sources_sha256, kernel_sources_sha256  # noqa: E402
 
 
 def git_head(root=ROOT):
+    """(commit, kernel sources unchanged from it?): run here, in the build container, on the PMC
+    passes copied back under profiles/ -- the GPU box has no .git (RCLONE_AMD_GIT_HEAD then)."""
     try:
-        return subprocess.check_output(["git", "-C", root, "rev-parse", "HEAD"], text=True).strip()
-    except Exception:  # noqa: BLE001 -- the GPU box has no .git
-        return os.environ.get("RCLONE_AMD_GIT_HEAD", "unknown")
+        head = subprocess.check_output(["git", "-C", root, "rev-parse", "HEAD"], text=True).strip()
+        clean = subprocess.run(["git", "-C", root, "diff", "--quiet", "HEAD", "--"] + KERNEL_SOURCES).returncode == 0
+        return head, clean
+    except Exception:  # noqa: BLE001
+        return os.environ.get("RCLONE_AMD_GIT_HEAD", "unknown"), None
 
 
 def main():
     d, out = sys.argv[1], sys.argv[2]
     acc = load(d)
-    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU / SQ_INSTS_VALU_MFMA_I8 ({d}), one pass per counter group, "
+    head, clean = git_head()
+    rel = os.path.relpath(os.path.abspath(d), ROOT)
+    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU / SQ_INSTS_VALU_MFMA_I8 ({rel}), one pass per counter group, "
                      "reads x2 (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md HBM section)",
            "blocks_per_launch": int(sys.argv[3]) if len(sys.argv) > 3 else 100_000,
            "kernel_sources_sha256": kernel_sources_sha256(),
            "kernel_sources": KERNEL_SOURCES,
-           "git_head": git_head()}
+           "git_head": head,
+           "kernel_sources_clean_at_git_head": clean,
+           "library_build_id": build_sources_sha256()}
     for k, cs in acc.items():
         for name, key in (("xs_seal", "seal"), ("xs_open", "open")):
             if name in k and "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
