@@ -56,6 +56,8 @@ def _load():
     lib.orc_simd_seal_blocks.restype = ctypes.c_int
     lib.orc_simd_open_blocks.argtypes = [vp, vp, vp, ctypes.c_int64, c_p, c_p]
     lib.orc_simd_open_blocks.restype = ctypes.c_int
+    lib.orc_simd_open_window.argtypes = [vp, vp, ctypes.c_size_t, c_p, c_p, ctypes.c_size_t, ctypes.c_size_t]
+    lib.orc_simd_open_window.restype = ctypes.c_int
     lib.orc_gen_block.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
     lib.orc_simd_seal_gen.argtypes = [vp, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, c_p, vp,
                                       c_p, vp]

@@ -407,3 +407,44 @@ int orc_simd_seal_gen(uint8_t *out, int64_t nblocks, uint64_t first, uint64_t st
   tagsum[1] = s1;
   return threads;
 }
+
+/* Windowed open, the CPU counterpart of a ranged read (cipher.go:972-1034 RangeSeek, then a short
+ * Read): the tag is verified over the whole block (secretbox.Open needs every ciphertext byte), but
+ * only the keystream blocks covering plaintext bytes [lo, hi) are generated and only those bytes of
+ * out are written.  Returns 0 when authentic, -1 otherwise (out untouched).  The reference's Go path
+ * decrypts the whole block (orc_simd_secretbox_open); this is the tuned CPU baseline beside the
+ * GPU's windowed open (tools/seek_latency.cpp over tests/native/cpu_engine.cpp). */
+int orc_simd_open_window(uint8_t *out, const uint8_t *box, size_t boxlen, const uint8_t nonce[24],
+                         const uint8_t key[32], size_t lo, size_t hi) {
+  const int level = orc_simd_level();
+  if (boxlen < 16) return -1;
+  const size_t n = boxlen - 16;
+  if (hi > n) hi = n;
+  uint8_t subkey[32], ks0[64], tag[16];
+  orc_hsalsa20(subkey, key, nonce);
+  uint32_t k[8];
+  for (int i = 0; i < 8; i++) k[i] = le32(subkey + 4 * i);
+  const uint32_t n0 = le32(nonce + 16), n1 = le32(nonce + 20);
+  uint8_t ks[16 * 64] __attribute__((aligned(64)));
+  if (level >= 2) salsa_x16(ks, k, n0, n1, 0);
+  else salsa_x8(ks, k, n0, n1, 0);
+  memcpy(ks0, ks, 64);
+  poly1305_44(tag, box + 16, n, ks0);
+  uint8_t diff = 0;
+  for (int i = 0; i < 16; i++) diff |= tag[i] ^ box[i];
+  if (diff) return -1;
+  if (lo >= hi) return 0;
+  /* plaintext byte i takes keystream byte i + 32 */
+  const size_t lanes = level >= 2 ? 16 : 8;
+  uint64_t blk = (lo + 32) / 64;
+  size_t i = lo;
+  while (i < hi) {
+    if (level >= 2) salsa_x16(ks, k, n0, n1, blk);
+    else salsa_x8(ks, k, n0, n1, blk);
+    const size_t base = (size_t)blk * 64; /* stream offset of ks[0] */
+    const size_t end = base + lanes * 64 - 32 < hi ? base + lanes * 64 - 32 : hi;
+    for (; i < end; i++) out[i] = box[16 + i] ^ ks[i + 32 - base];
+    blk += lanes;
+  }
+  return 0;
+}

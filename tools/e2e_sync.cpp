@@ -245,6 +245,11 @@ static int64_t mem_read(void* u, uint8_t* p, int64_t n, int32_t* err) {
 static int32_t mem_close(void*) { return RC_NIL; }
 
 static const int kSubdirs = 64;
+// which engine is behind the C ABI: librclone_crypt.so (the GPU), or the CPU baseline build of this
+// same harness over tests/native/cpu_engine.cpp (-DE2E_ENGINE=\"cpu\")
+#ifndef E2E_ENGINE
+#define E2E_ENGINE "gpu"
+#endif
 
 // EncryptFileName / DecryptFileName for every object in one batch (rc_names_run: one EME launch)
 static bool names_batch(rc_cipher* c, int32_t op, const std::vector<const std::string*>& in, std::vector<std::string>& out) {
@@ -716,7 +721,8 @@ int main(int argc, char** argv) {
   }
   const bool ok = failures == 0 && put_mismatch == 0 && ndiff == 0 && verify_bad == 0 && only_victim && name_mismatch == 0;
   const double g = (double)total / 1073741824.0;
-  printf("{\"config\": \"configs[4] e2e: sync local tree -> crypt(memory), cryptcheck\", \"mode\": \"%s\", "
+  printf("{\"config\": \"configs[4] e2e: sync local tree -> crypt(memory), cryptcheck\", \"engine\": \"" E2E_ENGINE "\", "
+         "\"mode\": \"%s\", "
          "\"tee\": \"%s\", \"check_mode\": \"%s\", \"checkers\": %d, "
          "\"objects\": %zu, \"gib\": %.3f, \"transfers\": %d, \"lanes\": %d, \"group_mib\": %llu, "
          "\"put_check\": \"%s\", \"hash_threads\": %d, "
@@ -727,7 +733,7 @@ int main(int argc, char** argv) {
          "\"name_mismatches\": %llu, \"example_remote_name\": \"%s\", "
          "\"anchored_objects\": %llu, \"devices\": \"%s\", \"tree_write_s\": %.2f, \"lane_seconds\": {\"sync_read\": %.3f, "
          "\"sync_gpu\": %.3f, \"check_read\": %.3f, \"check_gpu\": %.3f}, \"ok\": %s}\n",
-         mode.c_str(), mode == "stream" ? tee_mode.c_str() : "gpu", check_mode.c_str(), checkers, objs.size(), g, transfers, lanes, (unsigned long long)group_mib,
+         mode.c_str(), mode == "stream" ? tee_mode.c_str() : E2E_ENGINE, check_mode.c_str(), checkers, objs.size(), g, transfers, lanes, (unsigned long long)group_mib,
          check_dst ? put_check.c_str() : "off", hash_threads, t_sync, g / t_sync, t_puts, g / t_puts, t_dst, t_check, g / t_check, (unsigned long long)put_mismatch,
          (unsigned long long)ndiff, (unsigned long long)verified, (unsigned long long)verify_bad,
          (unsigned long long)flagged, t_names_enc, t_names_dec, (unsigned long long)name_mismatch,
