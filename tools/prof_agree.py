@@ -2,7 +2,7 @@
 """Compare rocprofv3 kernel-trace durations with bench.py's HIP-event averages for the same
 profiled command (tools/gpu_round.sh writes both).  The timed region is the last --steps
 launches of each kernel; the warmup launches before it are excluded, like bench.py does.
-usage: tools/prof_agree.py <prof_dir> <prof.log> <out.json> [steps]"""
+usage: tools/prof_agree.py <prof_dir> <prof.log> <out.json> [steps (default: the bench line's)]"""
 import csv
 import glob
 import json
@@ -11,7 +11,6 @@ import sys
 
 def main():
     d, log, out = sys.argv[1], sys.argv[2], sys.argv[3]
-    steps = int(sys.argv[4]) if len(sys.argv) > 4 else 10
     rows = []
     for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
         rows += list(csv.DictReader(open(f)))
@@ -19,6 +18,7 @@ def main():
     for line in open(log):
         if line.startswith("{"):
             bench = json.loads(line)
+    steps = int(sys.argv[4]) if len(sys.argv) > 4 else bench["steps"]  # the bench's own timed launches
     # the configs[3] leg (bench.py objectset_leg) runs after the headline timing: its launches
     # (warm-up + timed passes x rounds per pass) come last in the trace and are skipped
     tail = 0
