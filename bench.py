@@ -416,10 +416,14 @@ def headline_expected_digest(world, nb, independent):
         return None
     from rclone_amd.objectset import fullsize_pins
     hl = fullsize_pins()["bench_headline"]
-    if (hl["blocks_per_rank"], hl["seed"], hl["key"], hl["nonce0"]) != (nb, HEADLINE_SEED, HEADLINE_KEY.hex(),
-                                                                        HEADLINE_NONCE0.hex()):
+    if (hl["seed"], hl["key"], hl["nonce0"]) != (HEADLINE_SEED, HEADLINE_KEY.hex(), HEADLINE_NONCE0.hex()):
         return None
-    return hl["tag_digest"].get(str(world))
+    # the set is blocks 0 .. world*nb - 1 of one object whatever the split, and the digest is
+    # order-independent: the pin for k ranks of blocks_per_rank covers any world*nb equal to it
+    total, per = world * nb, hl["blocks_per_rank"]
+    if total % per:
+        return None
+    return hl["tag_digest"].get(str(total // per))
 
 
 def per_rank(dist, world, rank, dev, values):

@@ -183,4 +183,6 @@ def test_fail_if_wrong_paths():
     assert bench.headline_expected_digest(8, 100_000, False) != bench.headline_expected_digest(1, 100_000, False)
     assert bench.headline_expected_digest(3, 100_000, False) is None
     assert bench.headline_expected_digest(1, 50_000, False) is None
+    # the same blocks split another way: 4 ranks x 50 000 = blocks 0..199 999 = 2 ranks x 100 000
+    assert bench.headline_expected_digest(4, 50_000, False) == bench.headline_expected_digest(2, 100_000, False)
     assert bench.headline_expected_digest(1, 100_000, True) is None
