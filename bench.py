@@ -1077,6 +1077,27 @@ def main():
             b.record(stream)
             ev.append((False, a, b))
 
+    # correctness gate first, on one step: round trip + every tag verified + sampled blocks bit-exact
+    # against the oracle (rank 0 only; the oracle is the checker, never timed).  The warm-up then
+    # runs straight into the timed region, so the clock and the board power are settled when it
+    # starts (a host-side check between the two would let the GPU idle and cool)
+    step(False)
+    torch.cuda.synchronize(dev)
+    if not (torch.equal(out, plain) and int(ok.sum()) == nb):
+        raise SystemExit("bench: round trip failed on rank %d" % rank)
+    if rank == 0 and not args.no_cpu:
+        from oracle import pyoracle as orc
+        for j, i in enumerate([0, 1, nb // 2, nb - 1]):
+            p = plain[i * BLOCK_DATA:(i + 1) * BLOCK_DATA].cpu().numpy().tobytes()
+            w = body[i * BLOCK_SIZE:(i + 1) * BLOCK_SIZE].cpu().numpy().tobytes()
+            if orc.seal(p, block_nonce[j], key) != w:
+                raise SystemExit("bench: block %d differs from the oracle" % i)
+    # the clock probe runs at N=1 only (RCCL's own streams could share its hardware queue)
+    probe = ClockProbe(L, dev) if world == 1 else None
+    props = torch.cuda.get_device_properties(dev)
+    power = PowerSampler((props.pci_domain_id, props.pci_bus_id, props.pci_device_id))
+    if grouped(world):
+        dist.barrier()
     tw = time.perf_counter()
     nwarm, tail = 0, []
     while nwarm < args.warmup or time.perf_counter() - tw < args.warmup_seconds:
@@ -1088,23 +1109,8 @@ def main():
         nwarm += 4
     warm_s = time.perf_counter() - tw
     step_s = sorted(tail)[len(tail) // 2]  # settled per-step time: sizes the clock probe's window
-    # correctness gate before timing: round trip + every tag verified + sampled blocks
-    # bit-exact against the oracle (rank 0 only; the oracle is the checker, never timed)
-    if not (torch.equal(out, plain) and int(ok.sum()) == nb):
-        raise SystemExit("bench: round trip failed on rank %d" % rank)
-    if rank == 0 and not args.no_cpu:
-        from oracle import pyoracle as orc
-        for j, i in enumerate([0, 1, nb // 2, nb - 1]):
-            p = plain[i * BLOCK_DATA:(i + 1) * BLOCK_DATA].cpu().numpy().tobytes()
-            w = body[i * BLOCK_SIZE:(i + 1) * BLOCK_SIZE].cpu().numpy().tobytes()
-            if orc.seal(p, block_nonce[j], key) != w:
-                raise SystemExit("bench: block %d differs from the oracle" % i)
     if grouped(world):
         dist.barrier()
-    # the clock probe runs at N=1 only (RCCL's own streams could share its hardware queue)
-    probe = ClockProbe(L, dev) if world == 1 else None
-    props = torch.cuda.get_device_properties(dev)
-    power = PowerSampler((props.pci_domain_id, props.pci_bus_id, props.pci_device_id))
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     if probe:
@@ -1121,6 +1127,8 @@ def main():
     clock = probe.result() if probe else None
     if clock and el > 1.5 * args.steps * step_s:  # the probe must never have held the steps back
         clock["warning"] = f"timed region {el:.4f} s vs {args.steps * step_s:.4f} s expected"
+    if not torch.equal(out, plain):  # the last timed step's round trip (after the timing)
+        raise SystemExit("bench: round trip failed after the timed steps on rank %d" % rank)
     # counters and max time over ranks (RCCL, small tensors only)
     from rclone_amd.objectset import tag_digest
     counters = torch.tensor([args.steps * 2 * nb, args.steps * 2 * plain_len, int(nb - int(ok.sum())), 0, 0],
