@@ -55,14 +55,16 @@ def config3():
     # tag-fail injection in ~0.1% of the blocks
     nbad = max(3, len(d) // 1000)
     bad = np.sort(rng.choice(len(d), nbad, replace=False))
+    flips = []
     for j, b in enumerate(bad.tolist()):
         blen = 16 + int(d["len"][b])
         pos = [0, 15, 16, blen - 1, int(rng.integers(0, blen))][j % 5]
-        wire[int(d["dst"][b]) + pos] ^= 0x40
+        flips.append(int(d["dst"][b]) + pos)
+        wire[flips[-1]] ^= 0x40
     od = d.copy()
     od["src"], od["dst"] = d["dst"], d["src"]
     return dict(device=device, key=key, sizes=sizes, nonces=nonces, pstart=pstart, wstart=wstart, d=d, od=od,
-                obj=obj, bad=bad, plain_dev=plain_dev, plain_host=plain_host, wire=wire)
+                obj=obj, bad=bad, flips=flips, plain_dev=plain_dev, plain_host=plain_host, wire=wire)
 
 
 def test_config3_open_batch_flags_and_bytes(config3):
@@ -138,3 +140,19 @@ def test_config3_oracle_agrees_on_flags(config3):
     ok = np.zeros(len(od), dtype=np.uint8)
     orc.open_desc(out, ok, c["wire"], od, c["key"])
     assert np.array_equal(sample[ok == 0], c["bad"])
+
+
+def test_config3_gpu_seal_equals_the_oracle(config3):
+    # the other direction at full size: the same 10 GiB object set (partial last blocks, nonces
+    # that carry out of byte 7) sealed on the GPU in one descriptor batch (xs_seal_batch_dev,
+    # cipher.go:737 per block) equals the CPU oracle's wire image byte for byte -- the fixture's,
+    # with the injected flips undone
+    c = config3
+    body = torch.zeros(len(c["wire"]), dtype=torch.uint8, device="cuda")
+    c["device"].seal_batch(c["key"], c["d"], c["plain_dev"], body)
+    want = torch.from_numpy(c["wire"]).cuda()
+    want[torch.tensor(c["flips"], dtype=torch.int64, device="cuda")] ^= 0x40
+    torch.cuda.synchronize()
+    assert bool(torch.equal(body, want))
+    del body, want
+    torch.cuda.empty_cache()
