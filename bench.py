@@ -328,7 +328,8 @@ class PowerSampler:
         self.threading, self.period = threading, period
         self.dir = None
         dom, bus, dv = pci
-        for d in sorted(glob.glob(f"/sys/bus/pci/devices/{dom:04x}:{bus:02x}:{dv:02x}.0/hwmon/hwmon*")):
+        root = os.environ.get("RCLONE_AMD_SYSFS_ROOT") or "/sys"  # the library's sysfs root knob (tests)
+        for d in sorted(glob.glob(f"{root}/bus/pci/devices/{dom:04x}:{bus:02x}:{dv:02x}.0/hwmon/hwmon*")):
             if any(os.path.exists(os.path.join(d, f)) for f in ("power1_average", "power1_input")):
                 self.dir = d
                 break

@@ -186,3 +186,43 @@ def test_fail_if_wrong_paths():
     # the same blocks split another way: 4 ranks x 50 000 = blocks 0..199 999 = 2 ranks x 100 000
     assert bench.headline_expected_digest(4, 50_000, False) == bench.headline_expected_digest(2, 100_000, False)
     assert bench.headline_expected_digest(1, 100_000, True) is None
+
+
+def test_power_sampler_reads_hwmon(tmp_path, monkeypatch):
+    """bench.py's in-process board power / clock sampler over a fake amdgpu hwmon directory: the
+    mean of power1_input samples x the window, or the energy1_input difference when the counter
+    exists; None (with the reason) when the GPU has no hwmon power file."""
+    import importlib.util
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_pw", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    hw = tmp_path / "bus" / "pci" / "devices" / "0000:8b:00.0" / "hwmon" / "hwmon3"
+    hw.mkdir(parents=True)
+    (hw / "power1_input").write_text("1400000000\n")  # microwatts
+    (hw / "freq1_input").write_text("1850000000\n")   # Hz
+    monkeypatch.setenv("RCLONE_AMD_SYSFS_ROOT", str(tmp_path))
+    p = bench.PowerSampler((0, 0x8B, 0), period=0.002)
+    p.start()
+    time.sleep(0.1)
+    p.stop()
+    w, j, ghz, info = p.result()
+    assert w == 1400.0 and abs(ghz - 1.85) < 1e-9 and info["samples"] > 5
+    assert abs(j - 1400.0 * info["window_s"]) < 1400.0 * 1e-4  # window_s is rounded to 0.1 ms
+    assert bench.energy_per_gib([[0, 0, 0, w, j, ghz]], 2**30) == round(j, 4)
+    assert bench.energy_per_gib([[0, 0, 0, w, j, ghz], [0, 0, 0, None, None, None]], 2**30) is None
+    # an energy counter wins over sampled power
+    (hw / "energy1_input").write_text("5000000\n")  # microjoules
+    p = bench.PowerSampler((0, 0x8B, 0), period=0.002)
+    p.start()
+    (hw / "energy1_input").write_text("5700000\n")
+    time.sleep(0.02)
+    p.stop()
+    assert abs(p.result()[1] - 0.7) < 1e-9
+    # no such GPU in sysfs: nothing is read, the line says why
+    q = bench.PowerSampler((0, 0x99, 0))
+    q.start()
+    q.stop()
+    w, j, ghz, info = q.result()
+    assert w is None and j is None and "absent" in info["source"]
