@@ -108,16 +108,51 @@ std::mutex g_pool_mu;
 std::map<int, std::multimap<size_t, uint8_t*>>& g_pool = *new std::map<int, std::multimap<size_t, uint8_t*>>();
 size_t g_pool_cached = 0;
 
+// A buffer may serve a request of `bytes` when it is at least that large and not wastefully larger.
+inline bool fits(size_t cap, size_t bytes) { return cap >= bytes && cap <= 2 * bytes + (1u << 20); }
+
+// Per-thread front of the pool, as sync.Pool keeps a per-P private slot before its shared list: a
+// handle's buffers released on a thread are usually asked for again by the next handle on that
+// thread (a reader opening one ranged read after another), and with many threads the shared
+// pool's mutex was the point where 8 or 16 concurrent ranged readers stopped scaling (round 6,
+// DESIGN.md section 3e).  Bounded per thread; returned to the shared pool when the thread exits.
+constexpr int kTlsEntries = 6;
+constexpr size_t kTlsBytes = (size_t)32 << 20;
+struct TlsPool {
+  struct E {
+    uint8_t* p;
+    size_t cap;
+    int node;
+  } e[kTlsEntries];
+  int n = 0;
+  size_t bytes = 0;
+  ~TlsPool();
+};
+thread_local TlsPool t_pool;
+
 // Page-locked when possible.  If pinning fails (no device, pinned-memory limit) the buffer is plain
 // heap memory: a source that fails before its first block never needs the GPU, and the engine
 // stages pageable buffers through its own copies.
 uint8_t* pool_get(size_t bytes, size_t* cap, int node, bool* heap) {
   *heap = false;
+  {  // this thread's own cache first: no lock
+    TlsPool& t = t_pool;
+    int best = -1;
+    for (int i = 0; i < t.n; i++)
+      if (t.e[i].node == node && fits(t.e[i].cap, bytes) && (best < 0 || t.e[i].cap < t.e[best].cap)) best = i;
+    if (best >= 0) {
+      uint8_t* p = t.e[best].p;
+      *cap = t.e[best].cap;
+      t.bytes -= *cap;
+      t.e[best] = t.e[--t.n];
+      return p;
+    }
+  }
   {
     std::lock_guard<std::mutex> g(g_pool_mu);
     auto& m = g_pool[node];
     auto it = m.lower_bound(bytes);
-    if (it != m.end() && it->first <= 2 * bytes + (1u << 20)) {
+    if (it != m.end() && fits(it->first, bytes)) {
       *cap = it->first;
       uint8_t* p = it->second;
       g_pool_cached -= it->first;
@@ -141,6 +176,14 @@ void pool_put(uint8_t* p, size_t cap, int node, bool heap) {
     return;
   }
   {
+    TlsPool& t = t_pool;
+    if (t.n < kTlsEntries && t.bytes + cap <= kTlsBytes) {
+      t.e[t.n++] = {p, cap, node};
+      t.bytes += cap;
+      return;
+    }
+  }
+  {
     std::lock_guard<std::mutex> g(g_pool_mu);
     if (g_pool_cached + cap <= kPoolBytes) {
       g_pool[node].emplace(cap, p);
@@ -149,6 +192,18 @@ void pool_put(uint8_t* p, size_t cap, int node, bool heap) {
     }
   }
   xs_host_free(p);
+}
+
+// a thread's cached buffers go back to the shared pool when it exits; cached there whatever the
+// cap (never freed here: at process exit the HIP runtime may be going away)
+TlsPool::~TlsPool() {
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  for (int i = 0; i < n; i++) {
+    g_pool[e[i].node].emplace(e[i].cap, e[i].p);
+    g_pool_cached += e[i].cap;
+  }
+  n = 0;
+  bytes = 0;
 }
 
 struct PinnedBuf {
@@ -684,13 +739,14 @@ struct rc_decrypter {
 
 // staging for a full batch, allocated when the first block is read (not at open: a header
 // error or a failing source never needs it)
-static bool dec_alloc(rc_decrypter* fh) {
+// ... for `blocks` blocks: what this refill reads (a limited handle -- a ranged read -- needs one or
+// two blocks, not a whole read-ahead batch); grown when a later refill reads more
+static bool dec_alloc(rc_decrypter* fh, uint32_t blocks) {
   if (!fh->eng) fh->eng = xs_pool_next(cipher_pool(fh->c));  // staging goes on its GPU's node
   if (!fh->eng) return false;
-  const uint32_t batch = fh->c->batch_blocks;
   const int node = xs_engine_numa_node(fh->eng);
-  return fh->wire.ensure((size_t)batch * kBlockSize, node) && fh->plain.ensure((size_t)batch * kBlockData, node) &&
-         fh->okb.ensure(batch, node);
+  return fh->wire.ensure((size_t)blocks * kBlockSize, node) && fh->plain.ensure((size_t)blocks * kBlockData, node) &&
+         fh->okb.ensure(blocks, node);
 }
 
 // finish (cipher.go:1042-1052): sets the sticky error and returns it
@@ -729,7 +785,7 @@ static int32_t dec_close_locked(rc_decrypter* fh) {
 static int32_t dec_read_batch(rc_decrypter* fh, uint32_t want) {
   const uint32_t ra = next_batch(fh->c, fh->grow);
   if (want == 0 || want > ra) want = ra;
-  if (!dec_alloc(fh)) return RC_ERR_GPU;
+  if (!dec_alloc(fh, want)) return RC_ERR_GPU;
   const auto t0 = std::chrono::steady_clock::now();
   fh->blen.assign(want, 0);
   fh->berr.assign(want, RC_NIL);
