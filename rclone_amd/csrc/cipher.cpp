@@ -115,9 +115,13 @@ inline bool fits(size_t cap, size_t bytes) { return cap >= bytes && cap <= 2 * b
 // handle's buffers released on a thread are usually asked for again by the next handle on that
 // thread (a reader opening one ranged read after another), and with many threads the shared
 // pool's mutex was the point where 8 or 16 concurrent ranged readers stopped scaling (round 6,
-// DESIGN.md section 3e).  Bounded per thread; returned to the shared pool when the thread exits.
-constexpr int kTlsEntries = 6;
-constexpr size_t kTlsBytes = (size_t)32 << 20;
+// DESIGN.md section 3e).  Bounded per thread (a handle's two or three buffers) and over all
+// threads (a cgo caller may call in from many OS threads, and pinned memory is scarce); returned
+// to the shared pool when the thread exits.
+constexpr int kTlsEntries = 4;
+constexpr size_t kTlsBytes = (size_t)16 << 20;
+constexpr size_t kTlsTotalBytes = (size_t)512 << 20;
+std::atomic<size_t> g_tls_cached{0};
 struct TlsPool {
   struct E {
     uint8_t* p;
@@ -144,6 +148,7 @@ uint8_t* pool_get(size_t bytes, size_t* cap, int node, bool* heap) {
       uint8_t* p = t.e[best].p;
       *cap = t.e[best].cap;
       t.bytes -= *cap;
+      g_tls_cached.fetch_sub(*cap, std::memory_order_relaxed);
       t.e[best] = t.e[--t.n];
       return p;
     }
@@ -177,11 +182,13 @@ void pool_put(uint8_t* p, size_t cap, int node, bool heap) {
   }
   {
     TlsPool& t = t_pool;
-    if (t.n < kTlsEntries && t.bytes + cap <= kTlsBytes) {
+    if (t.n < kTlsEntries && t.bytes + cap <= kTlsBytes &&
+        g_tls_cached.fetch_add(cap, std::memory_order_relaxed) + cap <= kTlsTotalBytes) {
       t.e[t.n++] = {p, cap, node};
       t.bytes += cap;
       return;
     }
+    if (t.n < kTlsEntries && t.bytes + cap <= kTlsBytes) g_tls_cached.fetch_sub(cap, std::memory_order_relaxed);
   }
   {
     std::lock_guard<std::mutex> g(g_pool_mu);
@@ -197,6 +204,7 @@ void pool_put(uint8_t* p, size_t cap, int node, bool heap) {
 // a thread's cached buffers go back to the shared pool when it exits; cached there whatever the
 // cap (never freed here: at process exit the HIP runtime may be going away)
 TlsPool::~TlsPool() {
+  g_tls_cached.fetch_sub(bytes, std::memory_order_relaxed);
   std::lock_guard<std::mutex> g(g_pool_mu);
   for (int i = 0; i < n; i++) {
     g_pool[e[i].node].emplace(e[i].cap, e[i].p);
