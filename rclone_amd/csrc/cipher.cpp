@@ -73,19 +73,21 @@ int64_t read_fill(const rc_reader& r, uint8_t* buf, int64_t len, int32_t* err) {
 // node's GPUs (fs/sync/sync.go:544 startTransfers); a cipher may be bound to its own pool
 // (rc_cipher_set_pool).
 std::mutex g_pool_create_mu;
-xs_pool* g_xs_pool = nullptr;
+std::atomic<xs_pool*> g_xs_pool{nullptr};  // read without the lock once created (every refill asks)
 bool g_xs_pool_failed = false;
 
 xs_pool* process_pool() {
+  if (xs_pool* p = g_xs_pool.load(std::memory_order_acquire)) return p;
   std::lock_guard<std::mutex> g(g_pool_create_mu);
-  if (g_xs_pool || g_xs_pool_failed) return g_xs_pool;
+  if (g_xs_pool.load() || g_xs_pool_failed) return g_xs_pool.load();
   uint32_t batch = 256;
   if (const char* s = getenv("RCLONE_AMD_ENGINE_BLOCKS")) batch = (uint32_t)atoi(s);
   int slots = 3;  // combined batches in flight per engine
   if (const char* s = getenv("RCLONE_AMD_ENGINE_SLOTS")) slots = std::max(1, std::min(16, atoi(s)));
-  g_xs_pool = xs_pool_create(nullptr, 0, batch, slots);
-  if (!g_xs_pool) g_xs_pool_failed = true;
-  return g_xs_pool;
+  xs_pool* p = xs_pool_create(nullptr, 0, batch, slots);
+  if (!p) g_xs_pool_failed = true;
+  g_xs_pool.store(p, std::memory_order_release);
+  return p;
 }
 
 xs_pool* cipher_pool(const rc_cipher* c) { return c->pool ? c->pool : process_pool(); }
