@@ -131,6 +131,12 @@ xs_pool* xs_pool_create(const int*, int, uint32_t, int) {
 }
 void xs_pool_destroy(xs_pool* p) { delete p; }
 xs_engine* xs_pool_next(xs_pool* p) { return p ? &p->e[0] : nullptr; }
+xs_engine* xs_pool_engine(xs_pool* p, int i) { return p && i == 0 ? &p->e[0] : nullptr; }
+void xs_engine_stats(xs_engine* e, uint64_t out[3]) {  // one "batch" per call: no cross-caller combining
+  if (!e || !out) return;
+  out[0] = out[1] = e->calls.load();
+  out[2] = 0;
+}
 xs_engine* xs_engine_create(int, uint32_t, int) { return orc_simd_level() ? new xs_engine() : nullptr; }
 void xs_engine_destroy(xs_engine* e) { delete e; }
 

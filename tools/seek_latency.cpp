@@ -142,6 +142,9 @@ int main(int argc, char** argv) {
     std::vector<uint8_t> buf((size_t)len);
     for (int i = 0; i < 20; i++) one(rs, buf);
   }
+  uint64_t st0[3] = {0, 0, 0}, st1[3] = {0, 0, 0};  // engine: combined batches, requests, blocks
+  xs_engine* eng = xs_pool_engine(rc_default_pool(), 0);
+  xs_engine_stats(eng, st0);
   const double t0 = now();
   std::vector<std::thread> th;
   for (int t = 0; t < threads; t++)
@@ -152,6 +155,7 @@ int main(int argc, char** argv) {
     });
   for (auto& x : th) x.join();
   const double el = now() - t0;
+  xs_engine_stats(eng, st1);
   std::vector<double> all;
   for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
   std::sort(all.begin(), all.end());
@@ -161,6 +165,8 @@ int main(int argc, char** argv) {
   const double nr = (double)std::max<size_t>(all.size() + 20, 1);
   printf("\"mean_open_us\": %.1f, \"mean_read_us\": %.1f, \"mean_close_us\": %.1f, ", ph_open / nr, ph_read / nr,
          ph_close / nr);
+  printf("\"engine_batches\": %llu, \"engine_requests\": %llu, ", (unsigned long long)(st1[0] - st0[0]),
+         (unsigned long long)(st1[1] - st0[1]));
   printf("\"tool\": \"seek_latency\", \"object_mib\": %lld, \"read_len\": %lld, \"threads\": %d, \"reads\": %zu, "
          "\"p50_us\": %.1f, \"p90_us\": %.1f, \"p99_us\": %.1f, \"reads_per_s\": %.0f, \"bad\": %lld}\n",
          (long long)mib, (long long)len, threads, all.size(), pct(0.5), pct(0.9), pct(0.99), all.size() / el,
