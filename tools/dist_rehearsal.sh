@@ -24,6 +24,6 @@ run dist2_names --gpus 2 --steps 2 --warmup 1 --names 200000
 # configs[3] leg at world 8 (smaller headline share so eight ranks' buffers fit one GPU's HBM)
 if [ -n "$DIST8" ]; then
   run dist8 --gpus 8 --steps 2 --warmup 1 --warmup-seconds 0 --objectset-steps 0 --no-pool-check
-  run dist8_objset --gpus 8 --steps 2 --warmup 1 --warmup-seconds 0 --blocks 20000 --objectset-steps 1 --objectset-warmup 0 --no-pool-check
+  BENCH_OBJECTSET_ROUND_BLOCKS=50000 run dist8_objset --gpus 8 --steps 2 --warmup 1 --warmup-seconds 0 --blocks 20000 --objectset-steps 1 --objectset-warmup 0 --no-pool-check
 fi
 echo REHEARSAL_DONE
