@@ -1,3 +1,5 @@
+# ARCHIVED (round 6): ran the keygen-overlap A/B against a bench.py variant with BENCH_KEYGEN_SERIAL,
+# which was not kept (profiles/r06/keygen_overlap_ab/).
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=gpurun_out/r06s; mkdir -p $OUT
