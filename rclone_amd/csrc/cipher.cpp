@@ -747,10 +747,9 @@ struct rc_decrypter {
   int32_t wrapped = RC_NIL;
 };
 
-// staging for a full batch, allocated when the first block is read (not at open: a header
-// error or a failing source never needs it)
-// ... for `blocks` blocks: what this refill reads (a limited handle -- a ranged read -- needs one or
-// two blocks, not a whole read-ahead batch); grown when a later refill reads more
+// staging for the `blocks` blocks this refill reads (a limited handle -- a ranged read -- needs one
+// or two, not a whole read-ahead batch; grown when a later refill reads more), allocated when the
+// first block is read (not at open: a header error or a failing source never needs it)
 static bool dec_alloc(rc_decrypter* fh, uint32_t blocks) {
   if (!fh->eng) fh->eng = xs_pool_next(cipher_pool(fh->c));  // staging goes on its GPU's node
   if (!fh->eng) return false;
