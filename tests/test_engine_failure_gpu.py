@@ -65,11 +65,18 @@ def worker(t):
     for p in (inp, wire, out, ok):
         L.xs_host_free(p)
 
+# armed once; a round of the threads in which no batch of >= 2 requests formed (unlikely: they start
+# together at a barrier) leaves it armed and every call succeeding, and another round is run
 L.xs_test_fail_batch(2)
-th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
-[x.start() for x in th]
-[x.join() for x in th]
-failed_reqs = L.xs_test_failed_requests()
+for attempt in range(5):
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    [x.start() for x in th]
+    [x.join() for x in th]
+    failed_reqs = L.xs_test_failed_requests()
+    if failed_reqs:
+        break
+    bar.reset()
+R_done = attempt + 1
 # the engine still works after the failure
 plain = splitmix64_bytes(7, 3 * 65536)
 buf, body = L.xs_host_alloc(len(plain)), L.xs_host_alloc(len(plain) + 48)
@@ -80,7 +87,7 @@ st = (ctypes.c_uint64 * 3)()
 L.xs_engine_stats(e, st)
 L.xs_engine_destroy(e)
 fails = [c for c in calls if c[3] != 0]
-print(json.dumps({"calls": len(calls), "failed_reqs": failed_reqs, "fail_rcs": sorted({c[3] for c in fails}),
+print(json.dumps({"calls": len(calls), "rounds": R_done, "failed_reqs": failed_reqs, "fail_rcs": sorted({c[3] for c in fails}),
                   "nfail": len(fails), "fail_ops": sorted({c[2] for c in fails}),
                   "bad_success": [c[:3] for c in calls if c[3] == 0 and not c[4]][:10],
                   "after_ok": after, "batches": st[0], "requests": st[1]}))
@@ -101,7 +108,7 @@ def test_failed_combined_batch_reaches_every_follower(zero_copy):
     assert r.returncode == 0, r.stderr[-3000:]
     v = json.loads(r.stdout.strip().splitlines()[-1])
     print(v)
-    assert v["calls"] == 12 * 12 * 2
+    assert v["calls"] == 12 * 12 * 2 * v["rounds"]
     assert v["batches"] < v["requests"]  # requests did combine
     assert v["failed_reqs"] >= 2, v  # the hook fired on a combined batch
     assert v["nfail"] == v["failed_reqs"] and v["fail_rcs"] == [-2], v  # exactly its requests, XS_ERR_HIP
