@@ -58,6 +58,8 @@ def _load():
     lib.orc_simd_open_blocks.restype = ctypes.c_int
     lib.orc_simd_open_window.argtypes = [vp, vp, ctypes.c_size_t, c_p, c_p, ctypes.c_size_t, ctypes.c_size_t]
     lib.orc_simd_open_window.restype = ctypes.c_int
+    lib.orc_simd_encrypt_gen_file.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, c_p, c_p]
+    lib.orc_simd_encrypt_gen_file.restype = ctypes.c_int
     lib.orc_gen_block.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
     lib.orc_simd_seal_gen.argtypes = [vp, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, c_p, vp,
                                       c_p, vp]
@@ -229,3 +231,13 @@ def seal_gen(nblocks: int, first: int, stride: int, seed: int, nonce0: bytes, ke
     if threads == 0:
         raise RuntimeError("orc_simd_seal_gen needs AVX2")
     return (int(s[0]), int(s[1])), threads
+
+
+def encrypt_gen_file_into(buf, seed: int, size: int, nonce: bytes, key: bytes) -> int:
+    """The crypt file of the SplitMix64(seed) object of `size` bytes into buf (a writable numpy u8
+    array of at least encrypted_size(size) bytes); returns that size.  Releases the GIL (ctypes)."""
+    n = encrypted_size(size)
+    assert buf.nbytes >= n
+    if lib().orc_simd_encrypt_gen_file(buf.ctypes.data, seed, size, bytes(nonce), bytes(key)) != 0:
+        raise RuntimeError("orc_simd_encrypt_gen_file needs AVX2")
+    return n

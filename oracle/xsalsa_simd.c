@@ -448,3 +448,29 @@ int orc_simd_open_window(uint8_t *out, const uint8_t *box, size_t boxlen, const 
   }
   return 0;
 }
+
+/* The crypt file (cipher.go:694-758 encrypter: "RCLONE\0\0" || nonce || sealed blocks, block j with
+ * nonce + j) of an object whose plaintext is the SplitMix64 stream of `seed` (word k = mix(seed +
+ * (k+1)*golden), little-endian, truncated to `size` bytes: tools/e2e_sync.cpp's tree files,
+ * rclone_amd/testdata.py splitmix64_bytes).  out holds orc_encrypted_size(size) bytes.  Single
+ * threaded (callers run many objects at once).  Returns 0, or -1 when the CPU has no AVX2. */
+int orc_simd_encrypt_gen_file(uint8_t *out, uint64_t seed, uint64_t size, const uint8_t nonce0[24],
+                              const uint8_t key[32]) {
+  static const uint8_t magic[8] = {'R', 'C', 'L', 'O', 'N', 'E', 0, 0};
+  const int level = orc_simd_level();
+  if (level == 0) return -1;
+  memcpy(out, magic, 8);
+  memcpy(out + 8, nonce0, 24);
+  uint64_t w[SB_DATA / 8];
+  uint8_t *body = out + 32;
+  for (uint64_t j = 0; j * SB_DATA < size; j++) {
+    const uint64_t len = size - j * SB_DATA < SB_DATA ? size - j * SB_DATA : SB_DATA;
+    const uint64_t words = (len + 7) / 8, base = j * (SB_DATA / 8);
+    for (uint64_t i = 0; i < words; i++) w[i] = splitmix_word(seed, base + i);
+    uint8_t n[24];
+    memcpy(n, nonce0, 24);
+    orc_nonce_add(n, j);
+    seal_one(body + j * SB_SIZE, (const uint8_t *)w, len, n, key, level);
+  }
+  return 0;
+}

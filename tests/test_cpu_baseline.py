@@ -36,8 +36,10 @@ def test_cpu_engine_not_in_the_product():
                          ids=["batch", "stream"])
 def test_e2e_cpu_baseline_small(built, tmp_path, shape):
     anchor = str(tmp_path / "anchor.jsonl")
+    tee_all = str(tmp_path / "tee_all.txt")
     r = subprocess.run([os.path.join(built, "e2e_sync_cpu"), "--gib", "0.15", "--dir", str(tmp_path / "tree"),
-                        "--anchor", anchor] + shape, capture_output=True, text=True, timeout=600)
+                        "--anchor", anchor, "--tee-all", tee_all] + shape, capture_output=True, text=True,
+                       timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["engine"] == "cpu" and res["ok"] and res["corruption_flagged"] == 1
@@ -50,6 +52,9 @@ def test_e2e_cpu_baseline_small(built, tmp_path, shape):
         ct = orc.encrypt_file(splitmix64_bytes(row["seed"], row["size"]), bytes.fromhex(row["nonce"]), key)
         assert hashlib.sha256(ct).hexdigest() == row["sha256"], row
         assert hashlib.md5(ct).hexdigest() == row["tee_md5"], row
+    from tests.e2e_oracle import verify_tee_all
+    n, _, bad = verify_tee_all(tee_all, key)
+    assert n == res["objects"] == res["tee_listed"] and bad == []
 
 
 def test_seek_latency_cpu_small(built):

@@ -8,7 +8,10 @@ memory.go:580-588, crypt.go:784-852 + cmd/cryptcheck/cryptcheck.go:67-117).  Bes
 harness's own checks (put hash = remote hash, cryptcheck clean, sampled decrypts, the one
 corrupted object flagged), every sampled stored object -- the edge files, ~64 spread over the
 tree, the largest -- is recomputed here from its plaintext seed and stored nonce with the CPU
-oracle: SHA-256 of the whole crypt file and the MD5 crypt.put teed off the ciphertext.
+oracle: SHA-256 of the whole crypt file and the MD5 crypt.put teed off the ciphertext.  And every
+object of the tree (round 6): the harness lists each stored object's tee MD5 (--tee-all), which
+put's check already equated with the MD5 of the bytes the remote stored, and the vectorised
+oracle recomputes all of them (tests/e2e_oracle.py), so the whole 100 GiB is pinned, not a sample.
 
 Size: BASELINE configs[4]'s stated 100 GiB (RCLONE_AMD_E2E_GIB overrides).  It needs ~216 GiB
 of host memory -- the tree in /dev/shm plus the remote's pinned arena plus 4 x 4 GiB staging
@@ -90,10 +93,12 @@ def test_sync_cryptcheck_oracle_anchored(tmp_path, shape):
     base = "/dev/shm" if shm > gib + 4 else str(tmp_path)
     tree = os.path.join(base, "rc_e2e_anchor_%d" % os.getpid())
     anchor = str(tmp_path / "anchor.jsonl")
+    tee_all = str(tmp_path / "tee_all.txt")
     print(f"configs[4] e2e ({shape}) at {gib:.1f} GiB (tree in {base}, MemAvailable {_mem_available_gib():.0f} GiB)")
     try:
         # the harness's phase lines go to stderr as they happen (a long run shows progress)
-        r = subprocess.run([exe, "--gib", "%.3f" % gib, "--dir", tree, "--anchor", anchor] + SHAPES[shape],
+        r = subprocess.run([exe, "--gib", "%.3f" % gib, "--dir", tree, "--anchor", anchor, "--tee-all", tee_all] +
+                           SHAPES[shape],
                            stdout=subprocess.PIPE, text=True, timeout=800)
     finally:
         shutil.rmtree(tree, ignore_errors=True)
@@ -123,3 +128,12 @@ def test_sync_cryptcheck_oracle_anchored(tmp_path, shape):
         ct = orc.encrypt_file(plain, bytes.fromhex(row["nonce"]), key)
         assert hashlib.sha256(ct).hexdigest() == row["sha256"], (where, row)
         assert hashlib.md5(ct).hexdigest() == row["tee_md5"], (where, row)
+    # every object of the tree against the oracle (the tee MD5s; put's check tied them to the stored bytes)
+    import time
+
+    from tests.e2e_oracle import verify_tee_all
+    t0 = time.perf_counter()
+    n, nbytes, bad = verify_tee_all(tee_all, key)
+    print(f"configs[4] {shape}: all {n} stored objects ({nbytes / 2**30:.1f} GiB) equal the oracle's crypt files "
+          f"by MD5 ({time.perf_counter() - t0:.1f} s on the host)")
+    assert n == res["objects"] == res["tee_listed"] and bad == [], (where, bad[:10])

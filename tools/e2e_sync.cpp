@@ -41,13 +41,17 @@
 //            over the tree, the largest): plaintext seed and size, nonce, SHA-256 of the stored
 //            crypt file (header || wire body as the memory remote holds it) and the tee MD5 --
 //            tests/test_e2e_anchor_gpu.py recomputes them with the CPU oracle.
+//   tee-all: with --tee-all FILE, one text line per object ("index size seed nonce tee_md5", hex):
+//            every stored object's tee MD5, which put's check already equated with the MD5 of the
+//            bytes the remote stored -- tests/test_e2e_anchor_gpu.py recomputes all of them with the
+//            CPU oracle, so every stored byte of the tree is pinned, not a sample.
 //   devices: --devices 0,1,... puts lane l's engine on device list[l % n] and the rc_* handles
 //            and name engines on the same list (RCLONE_AMD_DEVICES): one process over several GPUs.
 //   usage: e2e_sync [--gib G] [--dir D] [--transfers T] [--mode batch|stream]
 //                   [--tee encrypter|reader] [--check-mode batch|stream] [--checkers C]
 //                   [--check-dst-hash 0|1] [--put-check inline|after] [--hash-threads H]
 //                   [--group-mib M] [--lanes L] [--keep]
-//                   [--anchor FILE] [--devices LIST]
+//                   [--anchor FILE] [--tee-all FILE] [--devices LIST]
 #include <fcntl.h>
 #include <sys/random.h>
 #include <sys/stat.h>
@@ -281,7 +285,7 @@ int main(int argc, char** argv) {
   std::string dir = "/tmp/rc_e2e_src", mode = "batch";
   int transfers = 16, check_dst = 1, keep = 0, nlanes = 4, checkers = 8, hash_threads = 0;
   uint64_t group_mib = 4096;
-  std::string anchor, devices, tee_mode = "encrypter", check_mode = "batch", put_check = "inline";
+  std::string anchor, tee_all, devices, tee_mode = "encrypter", check_mode = "batch", put_check = "inline";
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
     auto nx = [&] { return std::string(i + 1 < argc ? argv[++i] : ""); };
@@ -294,6 +298,7 @@ int main(int argc, char** argv) {
     else if (a == "--keep") keep = 1;
     else if (a == "--lanes") nlanes = std::max(1, atoi(nx().c_str()));
     else if (a == "--anchor") anchor = nx();
+    else if (a == "--tee-all") tee_all = nx();
     else if (a == "--devices") devices = nx();
     else if (a == "--tee") tee_mode = nx();
     else if (a == "--check-mode") check_mode = nx();
@@ -676,6 +681,21 @@ int main(int argc, char** argv) {
     if (n != o.size || memcmp(got.data(), want.data(), o.size) || (e != RC_EOF && e != RC_NIL)) verify_bad++;
     verified++;
   }
+  uint64_t tee_listed = 0;
+  if (!tee_all.empty()) {  // before the corruption below
+    FILE* f = fopen(tee_all.c_str(), "w");
+    if (!f) {
+      failures++;
+    } else {
+      for (size_t i = 0; i < objs.size(); i++) {
+        const Obj& o = objs[i];
+        fprintf(f, "%zu %llu %llu %s %s\n", i, (unsigned long long)o.size, (unsigned long long)(0xF11E0000ull + i),
+                hexs(o.header + 8, 24).c_str(), hexs(o.tee, 16).c_str());
+        tee_listed++;
+      }
+      fclose(f);
+    }
+  }
   uint64_t anchored = 0;
   if (!anchor.empty()) {  // before the corruption below: the objects as sync stored them
     std::vector<size_t> pick = {0, 1, 2, 3};
@@ -731,13 +751,13 @@ int main(int argc, char** argv) {
          "\"cryptcheck_differences\": %llu, \"verified_objects\": %llu, \"verify_failures\": %llu, "
          "\"corruption_flagged\": %llu, \"names_encrypt_s\": %.4f, \"names_decrypt_s\": %.4f, "
          "\"name_mismatches\": %llu, \"example_remote_name\": \"%s\", "
-         "\"anchored_objects\": %llu, \"devices\": \"%s\", \"tree_write_s\": %.2f, \"lane_seconds\": {\"sync_read\": %.3f, "
+         "\"anchored_objects\": %llu, \"tee_listed\": %llu, \"devices\": \"%s\", \"tree_write_s\": %.2f, \"lane_seconds\": {\"sync_read\": %.3f, "
          "\"sync_gpu\": %.3f, \"check_read\": %.3f, \"check_gpu\": %.3f}, \"ok\": %s}\n",
          mode.c_str(), mode == "stream" ? tee_mode.c_str() : E2E_ENGINE, check_mode.c_str(), checkers, objs.size(), g, transfers, lanes, (unsigned long long)group_mib,
          check_dst ? put_check.c_str() : "off", hash_threads, t_sync, g / t_sync, t_puts, g / t_puts, t_dst, t_check, g / t_check, (unsigned long long)put_mismatch,
          (unsigned long long)ndiff, (unsigned long long)verified, (unsigned long long)verify_bad,
          (unsigned long long)flagged, t_names_enc, t_names_dec, (unsigned long long)name_mismatch,
-         objs.empty() ? "" : objs.back().remote.c_str(), (unsigned long long)anchored, devices.c_str(), t_gen, sync_read, sync_gpu, check_read, check_gpu, ok ? "true" : "false");
+         objs.empty() ? "" : objs.back().remote.c_str(), (unsigned long long)anchored, (unsigned long long)tee_listed, devices.c_str(), t_gen, sync_read, sync_gpu, check_read, check_gpu, ok ? "true" : "false");
   for (int l = 0; l < lanes; l++) {
     xs_engine_destroy(eng[l]);
     xs_host_free(stage[l]);
